@@ -1,0 +1,116 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the C oracle (oracle/jsrt_oracle.c).
+
+The oracle is the CPU restatement of the reference render path used as the parity checker.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
+the product (jsraytracer_amd) never does.
+"""
+import ctypes
+import gzip
+import json
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libjsrt_oracle.so")
+GOLDEN = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("kind", ctypes.c_int32), ("seed", ctypes.c_uint32),
+                ("x_offset", ctypes.c_int32), ("x_delt", ctypes.c_int32), ("threads", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+STAT_FIELDS = ["samples", "color_calls", "casts", "object_tests", "node_visits", "tri_tests", "sdf_evals", "draws"]
+
+
+class OracleStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in STAT_FIELDS]
+
+
+def build():
+    """Compile the oracle with its own Makefile (gcc, strict IEEE)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.jsrt_oracle_render.restype = ctypes.c_int
+        L.jsrt_oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(OracleParams),
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(OracleStats)]
+        L.jsrt_oracle_last_error.restype = ctypes.c_char_p
+        L.jsrt_oracle_fmod.restype = ctypes.c_double
+        L.jsrt_oracle_fmod.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.jsrt_oracle_to_precision8.restype = ctypes.c_double
+        L.jsrt_oracle_to_precision8.argtypes = [ctypes.c_double]
+        L.jsrt_oracle_rng.restype = ctypes.c_double
+        L.jsrt_oracle_rng.argtypes = [ctypes.c_uint32] * 5
+        L.jsrt_oracle_mix.restype = ctypes.c_uint32
+        L.jsrt_oracle_mix.argtypes = [ctypes.c_uint32] * 2
+        _lib = L
+    return _lib
+
+
+def render(blob, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, threads=None):
+    """Render with the oracle. Returns (colors f32[H,W,4], rgba u8[H,W,4], stats dict)."""
+    L = lib()
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    p = OracleParams(width, height, spp, max_depth, kind, seed, x_offset, x_delt, threads, 0)
+    hdr = scene_header(blob)
+    W = width if width > 0 else hdr["width"]
+    H = height if height > 0 else hdr["height"]
+    colors = np.full((H, W, 4), np.nan, np.float32)
+    rgba = np.zeros((H, W, 4), np.uint8)
+    st = OracleStats()
+    buf = ctypes.create_string_buffer(bytes(blob), len(blob))
+    rc = L.jsrt_oracle_render(buf, len(blob), ctypes.byref(p), colors.ctypes.data, rgba.ctypes.data, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError("oracle: " + L.jsrt_oracle_last_error().decode())
+    return colors, rgba, {n: getattr(st, n) for n in STAT_FIELDS}
+
+
+def scene_header(blob):
+    """Minimal blob reader: renderer record fields (kind, spp, depth, width, height)."""
+    import struct
+    magic, version, nsec, _ = struct.unpack_from("<4I", blob, 0)
+    assert magic == 0x5452534A and version == 1
+    for i in range(nsec):
+        tag, count, off, nbytes = struct.unpack_from("<IIQQ", blob, 16 + 24 * i)
+        if tag == 0x52444E52:  # 'RNDR'
+            kind, spp, depth, w, h = struct.unpack_from("<5I", blob, off)
+            return {"kind": kind, "spp": spp, "max_depth": depth, "width": w, "height": h}
+    raise ValueError("no renderer record")
+
+
+# ---- golden fixtures (generated from the reference by oracle/refharness/regen_goldens.sh) ----
+def golden_index():
+    with open(os.path.join(GOLDEN, "index.json")) as f:
+        return json.load(f)["renders"]
+
+
+def golden_scene(name):
+    with gzip.open(os.path.join(GOLDEN, "scenes", name + ".jsrt.gz"), "rb") as f:
+        return f.read()
+
+
+def golden_image(tag, width, height):
+    rgba = np.fromfile(os.path.join(GOLDEN, "images", tag + ".rgba"), np.uint8).reshape(height, width, 4)
+    colors = np.fromfile(os.path.join(GOLDEN, "images", tag + ".f32"), np.float32).reshape(height, width, 4)
+    return colors, rgba
+
+
+def golden_kats():
+    with open(os.path.join(GOLDEN, "kats.json")) as f:
+        return json.load(f)
