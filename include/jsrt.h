@@ -1,0 +1,88 @@
+/*
+ * jsrt.h — C-ABI of libjsrt, the MI355X (gfx950) renderer that drops in for the reference's CPU
+ * web-worker render path.
+ *
+ * Reference interfaces replaced (alitteneker/jsraytracer):
+ *   jsrt_scene_create   <- the worker building its scene graph (src/worker.js:23-24 import +
+ *                          configureTest) and handing it to the renderer; the scene arrives as the
+ *                          JSRT blob of include/jsrt_scene.h (host exporter:
+ *                          jsraytracer_amd/js/scene_blob.js, in place of src/serializer.js:12-60)
+ *   jsrt_render         <- SimpleRenderer.render / IncrementalMultisamplingRenderer.render
+ *                          (src/renderers.js:10-41, 70-117): render(img, timelimit, callback,
+ *                          x_offset, x_delt) writing PixelBuffer RGBA8 (src/pixelbuffer.js:39-49),
+ *                          progress callback({pass, completion}) (renderers.js:35,110)
+ *   jsrt_render_device  <- same, device-resident outputs on a caller stream (multi-GPU tile path)
+ *   jsrt_scene_destroy  <- worker teardown (src/raytrace_launcher.js:106-124 terminate)
+ *   jsrt_last_error     <- the reference throws strings (e.g. src/aggregates.js:39); errors here are
+ *                          negative return codes + this message, never C++ exceptions.
+ *
+ * Threading: renders of one scene are re-entrant; each call uses its own device buffers.
+ * Ownership: the caller owns host output buffers; the library owns device memory and the scene.
+ */
+#ifndef JSRT_H
+#define JSRT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JSRT_ABI_VERSION 1
+
+typedef struct jsrt_scene jsrt_scene;
+
+typedef struct {
+    int32_t width, height;   /* <= 0: the blob's PixelBuffer size */
+    int32_t spp;             /* <= 0: renderer.samplesPerPixel from the blob */
+    int32_t max_depth;       /* <= 0: renderer.maxRecursionDepth from the blob */
+    int32_t kind;            /* < 0: blob's renderer; 0 Simple, 1 Incremental, 2 RandomMultisampling */
+    uint32_t seed;           /* keyed RNG seed (DESIGN.md "keyed RNG") */
+    int32_t x_offset, x_delt;/* reference column partition (renderers.js:21,88); x_delt <= 0 -> 1 */
+    int32_t device;          /* HIP device ordinal */
+    int32_t samples_per_launch; /* progressive chunking: samples per pixel per kernel launch (<=0: all) */
+    double timelimit_ms;     /* progress callback cadence (renderers.js:28-37); 0 = no callback */
+    int32_t reserved[6];
+} jsrt_params;
+
+typedef struct {
+    double kernel_ms;        /* sum of render-kernel durations (HIP events on the render stream) */
+    double total_ms;         /* host wall time of the call */
+    uint64_t samples;        /* pixel-samples rendered */
+    uint32_t launches;       /* render-kernel launches */
+    uint32_t reserved0;
+    double reserved[4];
+} jsrt_stats;
+
+typedef void (*jsrt_progress_fn)(int32_t pass, double completion, void *user);
+
+/* Parse + validate a JSRT blob and upload it to `device`. Returns 0 or negative. */
+int jsrt_scene_create(const void *scene_blob, size_t n, int32_t device, jsrt_scene **out);
+void jsrt_scene_destroy(jsrt_scene *scene);
+
+/* Render into host buffers.  rgba8 (W*H*4 bytes) receives the PixelBuffer bytes of the rendered
+ * columns only (other columns untouched, as each reference worker leaves them); colors_f32
+ * (W*H*4, nullable) the final f32 colour handed to setColor (alpha 1).  progress may be NULL. */
+int jsrt_render(jsrt_scene *scene, const jsrt_params *params, uint8_t *rgba8, float *colors_f32,
+                jsrt_progress_fn progress, void *user, jsrt_stats *stats);
+
+/* Render the owned columns into DEVICE buffers on `hip_stream` (a hipStream_t, 0 = null stream).
+ * Owned columns: px >= x_offset, (px - x_offset) % x_delt == 0, packed in order: owned column c,
+ * row py lives at [(c * H + py)] of d_rgba8 (u32 RGBA8) and d_colors (f32x4, nullable).
+ * col_block > 1 assigns blocks of col_block columns round-robin (rank = (px / col_block) % x_delt
+ * == x_offset) for coherent multi-GPU tiles.  Asynchronous w.r.t. the host. */
+int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
+                       float *d_colors, void *hip_stream, jsrt_stats *stats);
+
+/* Number of owned columns for (W, x_offset, x_delt, col_block). */
+int32_t jsrt_owned_columns(int32_t width, int32_t x_offset, int32_t x_delt, int32_t col_block);
+
+const char *jsrt_last_error(void);
+int32_t jsrt_abi_version(void);
+/* Device count visible to HIP (0 without a GPU); never initialises a context it does not need. */
+int32_t jsrt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

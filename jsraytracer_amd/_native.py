@@ -1,0 +1,84 @@
+"""ctypes binding of libjsrt.so (include/jsrt.h).
+
+The library is built in-tree (jsraytracer_amd/_build/libjsrt.so, see build.py) so the GPU box loads
+exactly the code object compiled here.  There is no CPU fallback: if the library or a HIP device is
+missing, every render entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libjsrt.so")
+
+
+class JsrtError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("kind", ctypes.c_int32), ("seed", ctypes.c_uint32),
+                ("x_offset", ctypes.c_int32), ("x_delt", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("samples_per_launch", ctypes.c_int32), ("timelimit_ms", ctypes.c_double),
+                ("reserved", ctypes.c_int32 * 6)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("samples", ctypes.c_uint64),
+                ("launches", ctypes.c_uint32), ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_double * 4)]
+
+    def as_dict(self):
+        return {"kernel_ms": self.kernel_ms, "total_ms": self.total_ms, "samples": int(self.samples),
+                "launches": int(self.launches)}
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)
+
+# exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
+EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_owned_columns",
+           "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
+
+_lib = None
+
+
+def lib():
+    """Load libjsrt.so (raises JsrtError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 (same SONAME as
+    # /opt/rocm's).  Loading torch first makes libjsrt bind to that already-loaded copy, so torch
+    # tensors/streams/RCCL and libjsrt share one runtime (loading ours first breaks torch.cuda).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise JsrtError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__; __graft_entry__.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    L.jsrt_scene_create.restype = ctypes.c_int
+    L.jsrt_scene_create.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]
+    L.jsrt_scene_destroy.restype = None
+    L.jsrt_scene_destroy.argtypes = [ctypes.c_void_p]
+    L.jsrt_render.restype = ctypes.c_int
+    L.jsrt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_void_p,
+                              PROGRESS_FN, ctypes.c_void_p, ctypes.POINTER(Stats)]
+    L.jsrt_render_device.restype = ctypes.c_int
+    L.jsrt_render_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
+    L.jsrt_owned_columns.restype = ctypes.c_int32
+    L.jsrt_owned_columns.argtypes = [ctypes.c_int32] * 4
+    L.jsrt_last_error.restype = ctypes.c_char_p
+    L.jsrt_abi_version.restype = ctypes.c_int32
+    L.jsrt_device_count.restype = ctypes.c_int32
+    _lib = L
+    return L
+
+
+def last_error():
+    return lib().jsrt_last_error().decode(errors="replace")
+
+
+def check(rc, what):
+    if rc != 0:
+        raise JsrtError(f"{what} failed ({rc}): {last_error()}")

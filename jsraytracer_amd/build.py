@@ -1,0 +1,44 @@
+"""Builds libjsrt.so in-tree with hipcc for gfx950 (no JIT caches: the .so travels to the GPU box)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT, "libjsrt.so")
+SOURCES = ["render.hip", "capi.cpp", "scene_load.cpp"]
+HEADERS = ["device_scene.h", "render_kernel.h", "scene_load.h", "sdf_program.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")
+
+# Strict IEEE (the reference's numeric model): no FMA contraction, no fast-math,
+# f32 denormals preserved (HIP's default), correctly rounded f32 div/sqrt (HIP's default).
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+         "-Wall", "-Wno-unused-function"]
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps += [os.path.join(HERE, "..", "include", f) for f in ("jsrt.h", "jsrt_scene.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OUT, exist_ok=True)
+    if not force and not _stale():
+        return LIB
+    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)

@@ -1,0 +1,296 @@
+// capi.cpp — the C-ABI of include/jsrt.h: scene upload, render launches, host/device outputs.
+//
+// No C++ exception crosses the ABI; every entry point returns 0 / negative and records a message
+// for jsrt_last_error() (the reference throws strings, e.g. src/aggregates.js:39).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/jsrt.h"
+#include "render_kernel.h"
+#include "scene_load.h"
+
+using namespace jsrt;
+
+namespace {
+thread_local std::string g_err;
+int set_error(int code, const std::string &m) {
+    g_err = m;
+    return code;
+}
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return set_error(-3, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DeviceArena {  // one allocation holding every scene array (256-B aligned pieces)
+    std::vector<uint8_t> host;
+    size_t add(const void *p, size_t bytes) {
+        size_t off = (host.size() + 255) & ~(size_t)255;
+        host.resize(off + bytes);
+        if (bytes) memcpy(host.data() + off, p, bytes);
+        return off;
+    }
+    template <class T>
+    size_t add(const std::vector<T> &v) { return add(v.data(), v.size() * sizeof(T)); }
+};
+}  // namespace
+
+struct jsrt_scene {
+    int device = 0;
+    void *dmem = nullptr;
+    DScene ds;
+    HostScene hs;
+};
+
+extern "C" {
+
+int32_t jsrt_abi_version(void) { return JSRT_ABI_VERSION; }
+const char *jsrt_last_error(void) { return g_err.c_str(); }
+
+int32_t jsrt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int32_t jsrt_owned_columns(int32_t width, int32_t x_offset, int32_t x_delt, int32_t col_block) {
+    if (width <= 0) return 0;
+    if (x_delt <= 0) x_delt = 1;
+    int32_t n = 0;
+    if (col_block <= 1) {
+        for (int32_t px = x_offset; px < width; px += x_delt) ++n;
+        return n;
+    }
+    for (int32_t c = 0;; ++c) {
+        if (owned_to_px(c, x_offset, x_delt, col_block) >= width) {
+            // columns of a block are consecutive; stop at the first out-of-range one
+            return n;
+        }
+        ++n;
+    }
+}
+
+int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **out) {
+    if (!out) return set_error(-1, "out is NULL");
+    *out = nullptr;
+    std::unique_ptr<jsrt_scene> sc(new jsrt_scene());
+    std::string err;
+    if (load_scene(blob, n, sc->hs, err)) return set_error(-2, err);
+    HostScene &H = sc->hs;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_error(-3, "no such HIP device");
+    HIP_TRY(hipSetDevice(device));
+    sc->device = device;
+    DeviceArena A;
+    const size_t o_prims = A.add(H.prims), o_insts = A.add(H.insts), o_ichild = A.add(H.inst_child),
+                 o_roots = A.add(H.roots), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
+                 o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
+                 o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
+                 o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
+                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg);
+    const size_t total = A.host.size() + 256;
+    HIP_TRY(hipMalloc(&sc->dmem, total));
+    HIP_TRY(hipMemcpy(sc->dmem, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
+    uint8_t *b = static_cast<uint8_t *>(sc->dmem);
+    DScene &D = sc->ds;
+    memset(&D, 0, sizeof D);
+    D.prims = (const DPrim *)(b + o_prims);
+    D.insts = (const DInst *)(b + o_insts);
+    D.inst_child = (const int32_t *)(b + o_ichild);
+    D.roots = (const int32_t *)(b + o_roots);
+    D.mats = (const double *)(b + o_mats);
+    D.ctx = (const double *)(b + o_ctx);
+    D.bvh = (const DBvhNode *)(b + o_bvh);
+    D.leaf_prims = (const int32_t *)(b + o_lp);
+    D.leaf_tris = (const int32_t *)(b + o_lt);
+    D.tris = (const DTri *)(b + o_tris);
+    D.trish = (const DTriShade *)(b + o_trish);
+    D.mat = (const jsrt_rec_material *)(b + o_mat);
+    D.mc = (const jsrt_rec_mcolor *)(b + o_mc);
+    D.lights = (const DLight *)(b + o_lights);
+    D.sdf_insn = (const SdfInsn *)(b + o_insn);
+    D.sdf_const = (const double *)(b + o_const);
+    D.sdf_range = (const int32_t *)(b + o_range);
+    D.sdf_child = (const int32_t *)(b + o_schild);
+    D.sdf_nodes = (const jsrt_rec_sdfnode *)(b + o_snodes);
+    D.sdfg = (const jsrt_rec_sdfgeom *)(b + o_sdfg);
+    D.n_roots = (int32_t)H.roots.size();
+    D.n_lights = (int32_t)H.lights.size();
+    D.n_prims = (int32_t)H.prims.size();
+    D.n_insts = (int32_t)H.insts.size();
+    D.cam = H.cam;
+    memcpy(D.bg, H.bg, sizeof D.bg);
+    D.all_roots_prims = H.all_roots_prims;
+    *out = sc.release();
+    return 0;
+}
+
+void jsrt_scene_destroy(jsrt_scene *s) {
+    if (!s) return;
+    if (s->dmem) {
+        (void)hipSetDevice(s->device);
+        (void)hipFree(s->dmem);
+    }
+    delete s;
+}
+
+}  // extern "C"
+
+namespace {
+
+struct Resolved {
+    RenderArgs a;
+    int32_t col_block;
+};
+
+int resolve(const jsrt_scene *s, const jsrt_params *p, int32_t col_block, Resolved &R) {
+    if (!s) return set_error(-1, "scene is NULL");
+    const HostScene &H = s->hs;
+    RenderArgs &a = R.a;
+    memset(&a, 0, sizeof a);
+    a.W = p && p->width > 0 ? p->width : H.width;
+    a.H = p && p->height > 0 ? p->height : H.height;
+    a.spp = p && p->spp > 0 ? p->spp : H.spp;
+    a.max_depth = p && p->max_depth > 0 ? p->max_depth : H.max_depth;
+    a.kind = p && p->kind >= 0 ? p->kind : H.kind;
+    a.seed = p ? p->seed : 1u;
+    a.x_offset = p ? p->x_offset : 0;
+    a.x_delt = p && p->x_delt > 0 ? p->x_delt : 1;
+    if (a.W <= 0 || a.H <= 0) return set_error(-1, "image size must be positive");
+    if (a.kind < 0 || a.kind > 2) return set_error(-1, "unknown renderer kind");
+    if (a.kind == JSRT_RENDERER_SIMPLE) a.spp = 1;
+    if (a.spp <= 0) return set_error(-1, "samplesPerPixel must be positive");
+    if (a.max_depth < 0 || a.max_depth > MAX_TREE_DEPTH)
+        return set_error(-1, "maxRecursionDepth above " + std::to_string(MAX_TREE_DEPTH) + " is not supported");
+    if (a.x_offset < 0) return set_error(-1, "x_offset must be >= 0");
+    if (col_block > 1 && a.x_offset >= a.x_delt) return set_error(-1, "block partition needs x_offset < x_delt");
+    R.col_block = col_block > 1 ? col_block : 1;
+    a.col_block = R.col_block;
+    a.ncols = jsrt_owned_columns(a.W, a.x_offset, a.x_delt, R.col_block);
+    a.patches_x = (a.ncols + 7) / 8;
+    a.patches = a.patches_x * ((a.H + 7) / 8);
+    return 0;
+}
+
+// Runs the launch sequence (chunked by samples_per_launch) on `stream`, timing every launch with
+// HIP events recorded on that stream.
+int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_rgba, float *d_colors,
+                 hipStream_t stream, jsrt_progress_fn progress, void *user, jsrt_stats *st) {
+    const int per = (p && p->samples_per_launch > 0) ? p->samples_per_launch : a.spp;
+    const int nl = (a.spp + per - 1) / per;
+    float *accum = nullptr;
+    if (nl > 1) HIP_TRY(hipMallocAsync((void **)&accum, (size_t)a.ncols * a.H * 4 * sizeof(float), stream));
+    std::vector<hipEvent_t> ev(2 * (size_t)nl);
+    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    a.rgba = d_rgba;
+    a.colors = d_colors;
+    a.accum = accum;
+    auto t_last = std::chrono::steady_clock::now();
+    const double tl = p ? p->timelimit_ms : 0;
+    int rc = 0;
+    for (int l = 0; l < nl && !rc; ++l) {
+        a.s_begin = l * per;
+        a.s_end = std::min(a.spp, a.s_begin + per);
+        a.final_pass = (l == nl - 1);
+        if (hipEventRecord(ev[2 * l], stream) != hipSuccess) rc = set_error(-3, "hipEventRecord");
+        hipError_t e = launch_render(s->ds, a, stream);
+        if (e != hipSuccess) { rc = set_error(-3, std::string("render launch: ") + hipGetErrorString(e)); break; }
+        if (hipEventRecord(ev[2 * l + 1], stream) != hipSuccess) rc = set_error(-3, "hipEventRecord");
+        if (progress && tl > 0 && l + 1 < nl) {  // renderers.js:103-112 cadence, at launch granularity
+            if (hipStreamSynchronize(stream) != hipSuccess) { rc = set_error(-3, "render failed"); break; }
+            auto now = std::chrono::steady_clock::now();
+            if (std::chrono::duration<double, std::milli>(now - t_last).count() >= tl) {
+                t_last = now;
+                progress(a.s_end - 1, (double)a.s_end / a.spp, user);
+            }
+        }
+    }
+    if (!rc && st) {
+        if (hipStreamSynchronize(stream) != hipSuccess) rc = set_error(-3, "render kernel failed");
+        double ms = 0;
+        for (int l = 0; l < nl && !rc; ++l) {
+            float x = 0;
+            if (hipEventElapsedTime(&x, ev[2 * l], ev[2 * l + 1]) == hipSuccess) ms += x;
+        }
+        st->kernel_ms = ms;
+        st->launches = (uint32_t)nl;
+        st->samples = (uint64_t)a.ncols * a.H * a.spp;
+    }
+    if (accum) (void)hipFreeAsync(accum, stream);
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int jsrt_render(jsrt_scene *s, const jsrt_params *p, uint8_t *rgba8, float *colors_f32, jsrt_progress_fn progress,
+                void *user, jsrt_stats *stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Resolved R;
+    if (int rc = resolve(s, p, 1, R)) return rc;
+    if (!rgba8) return set_error(-1, "rgba8 is NULL");
+    RenderArgs &a = R.a;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t stream;
+    HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    const size_t npx = (size_t)a.ncols * a.H;
+    uint32_t *d_rgba = nullptr;
+    float *d_col = nullptr;
+    int rc = 0;
+    jsrt_stats st;
+    memset(&st, 0, sizeof st);
+    if (hipMalloc(&d_rgba, npx * 4) != hipSuccess) rc = set_error(-3, "out of device memory");
+    if (!rc && colors_f32 && hipMalloc(&d_col, npx * 16) != hipSuccess) rc = set_error(-3, "out of device memory");
+    if (!rc) rc = run_launches(s, p, a, d_rgba, d_col, stream, progress, user, &st);
+    if (!rc && npx) {
+        std::vector<uint32_t> h_rgba(npx);
+        std::vector<float> h_col(colors_f32 ? npx * 4 : 0);
+        if (hipMemcpyAsync(h_rgba.data(), d_rgba, npx * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+            (colors_f32 && hipMemcpyAsync(h_col.data(), d_col, npx * 16, hipMemcpyDeviceToHost, stream) != hipSuccess) ||
+            hipStreamSynchronize(stream) != hipSuccess)
+            rc = set_error(-3, "device-to-host copy failed");
+        if (!rc) {  // owned column c, row py -> image (px, py); other columns untouched (worker.js semantics)
+            for (int32_t c = 0; c < a.ncols; ++c) {
+                const int32_t px = owned_to_px(c, a.x_offset, a.x_delt, 1);
+                for (int32_t py = 0; py < a.H; ++py) {
+                    const size_t src = (size_t)c * a.H + py, dst = (size_t)py * a.W + px;
+                    memcpy(rgba8 + 4 * dst, &h_rgba[src], 4);
+                    if (colors_f32) memcpy(colors_f32 + 4 * dst, &h_col[4 * src], 16);
+                }
+            }
+        }
+    }
+    if (d_rgba) (void)hipFree(d_rgba);
+    if (d_col) (void)hipFree(d_col);
+    (void)hipStreamDestroy(stream);
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = st;
+    return rc;
+}
+
+int jsrt_render_device(jsrt_scene *s, const jsrt_params *p, int32_t col_block, uint32_t *d_rgba8, float *d_colors,
+                       void *hip_stream, jsrt_stats *stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Resolved R;
+    if (int rc = resolve(s, p, col_block, R)) return rc;
+    if (!d_rgba8) return set_error(-1, "d_rgba8 is NULL");
+    HIP_TRY(hipSetDevice(s->device));
+    jsrt_stats st;
+    memset(&st, 0, sizeof st);
+    const int rc = run_launches(s, p, R.a, d_rgba8, d_colors, (hipStream_t)hip_stream, nullptr, nullptr,
+                                stats ? &st : nullptr);
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = st;
+    return rc;
+}
+
+}  // extern "C"

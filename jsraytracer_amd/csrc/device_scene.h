@@ -1,0 +1,112 @@
+// device_scene.h — HBM layout of a loaded scene (built by scene_load.cpp from a JSRT blob).
+//
+// Everything the render kernel reads lives in ONE device allocation; DScene carries the device
+// pointers by value as a kernel argument (scalar-cache loads).  Layout choices:
+//   * top-level objects are walked in World.objects order by every lane together (wave-uniform
+//     loop, world.js:7-15), so per-object records are read through the scalar path;
+//   * BVH nodes are 32-byte records (center f32x3 | child/leaf word | half f32x3 | child/leaf word),
+//     one 32-B sector per node visit, visited greater-child-first as aggregates.js:221-222;
+//   * triangles are 96-byte records holding exactly the fields Triangle.intersect reads
+//     (geometry.js:368-375: normal, delta, p0, v0, v1, d00/d01/d11/denom), shading-only data
+//     (vertex normals, UVs) lives in a separate array touched once per hit.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/jsrt_scene.h"
+#include "sdf_program.h"
+
+namespace jsrt {
+
+enum : int32_t { INST_PRIM = 1, INST_AGG = 2, INST_BVH = 3 };
+
+struct DPrim {           // world.js:104 Primitive
+    double inv[12];      // inv_transform rows 0..2 (row 3 verified == 0,0,0,1 at load)
+    int32_t gkind;       // JSRT_GEOM_*
+    int32_t gindex;      // triangle / sdf-geometry index
+    int32_t material;    // MATL index
+    int32_t casts_shadow;
+    float center[4];     // AABB geometry (geometry.js:77)
+    float half[4];
+};
+static_assert(sizeof(DPrim) == 144, "DPrim");
+
+struct DInst {           // one node of the object tree flattened per path (shared DAG nodes duplicated)
+    int32_t kind;        // INST_*
+    int32_t prim;        // INST_PRIM: DPrim index
+    int32_t first;       // INST_AGG: first child in inst_child[]; INST_BVH: root node
+    int32_t count;       // INST_AGG: child count; INST_BVH: 1 if every leaf object is an identity-
+                         //           transform, shadow-casting triangle Primitive (fast leaf path)
+    int32_t matrix;      // AGG/BVH: index of the object's inverse matrix in mats[] (12 doubles)
+    int32_t ctx;         // AGG/BVH: shading context id of everything below it
+    int32_t pad[2];
+};
+
+struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
+    float cx, cy, cz;
+    int32_t a;           // internal: lesser child; leaf: first index into leaf_prims[]
+    float hx, hy, hz;
+    int32_t b;           // internal: greater child (>= 0); leaf: ~count (< 0)
+};
+static_assert(sizeof(DBvhNode) == 32, "DBvhNode");
+
+struct DTri {            // geometry.js:334-354 Triangle (intersection fields)
+    float n[3];          // this.normal (w = 0)
+    float p0[3];         // ps[0] xyz (w = 1)
+    float v0[3], v1[3];  // ps[1]-ps[0], ps[2]-ps[0] (to3)
+    double delta, d00, d11, d01, denom;
+    int32_t prim;        // owning DPrim (for shading / materials)
+    int32_t shade;       // index into DTriShade or -1
+};
+static_assert(sizeof(DTri) == 96, "DTri");
+
+struct DTriShade {       // Triangle.psdata (objloader.js:198-201): vertex normals / UVs
+    float vn[3][4];
+    float uv[3][4];
+    int32_t has_normal, has_uv, uv_len, pad;
+};
+
+struct DLight {          // lights.js:27 / :56
+    int32_t kind, color, gkind, samples;
+    float pos[3];        // point light position (xyz)
+    int32_t pos_len;
+    float wn[4];         // area light over a plane-like surface: world normal, precomputed exactly
+    int32_t needs_uv;    // colour depends on UV (a checkerboard in its MaterialColor chain)
+    int32_t pad2[3];
+    double T[16], Ti[16];
+};
+
+struct DCamera {         // cameras.js:18-53
+    double T[16];
+    double tan_fov, aspect, focus, sensor;
+    int32_t kind, pad[3];
+};
+
+struct DScene {
+    const DPrim *prims;
+    const DInst *insts;
+    const int32_t *inst_child;
+    const int32_t *roots;
+    const double *mats;      // 12 doubles per AGG/BVH instance matrix
+    const double *ctx;       // 16 doubles per shading context (ctx 0 = identity)
+    const DBvhNode *bvh;
+    const int32_t *leaf_prims;   // DPrim indices (generic leaves)
+    const int32_t *leaf_tris;    // DTri indices (fast leaves), parallel to leaf_prims
+    const DTri *tris;
+    const DTriShade *trish;
+    const jsrt_rec_material *mat;
+    const jsrt_rec_mcolor *mc;
+    const DLight *lights;
+    const SdfInsn *sdf_insn;     // SDF programs (sdf_program.h)
+    const double *sdf_const;
+    const int32_t *sdf_range;    // [2*node]: code range of SDF node `node`
+    const int32_t *sdf_child;    // child lists of SDF union/intersection nodes (blob CHLD)
+    const jsrt_rec_sdfnode *sdf_nodes;
+    const jsrt_rec_sdfgeom *sdfg;
+    int32_t n_roots, n_lights, n_prims, n_insts;
+    DCamera cam;
+    float bg[4];
+    int32_t all_roots_prims; // every root is an INST_PRIM (uniform fast path)
+    int32_t pad[3];
+};
+
+}  // namespace jsrt

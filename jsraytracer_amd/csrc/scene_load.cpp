@@ -1,0 +1,587 @@
+// scene_load.cpp — parse + validate a JSRT blob (include/jsrt_scene.h) into the HBM layout of
+// device_scene.h.  Host-only; compiled with -ffp-contract=off so the few float64 values computed
+// here (shading contexts, area-light normals) round exactly as the reference's JS does.
+#include "scene_load.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <map>
+#include <unordered_map>
+
+namespace jsrt {
+namespace {
+
+struct Blob {
+    const jsrt_rec_renderer *rndr = nullptr;
+    const jsrt_rec_camera *cam = nullptr;
+    const jsrt_rec_mcolor *mc = nullptr;
+    const jsrt_rec_material *mat = nullptr;
+    const jsrt_rec_geometry *geom = nullptr;
+    const jsrt_rec_object *obj = nullptr;
+    const jsrt_rec_matrix *mats = nullptr;
+    const int32_t *root = nullptr, *chld = nullptr;
+    const jsrt_rec_bvhnode *bvh = nullptr;
+    const jsrt_rec_triangle *tri = nullptr;
+    const jsrt_rec_light *lite = nullptr;
+    const jsrt_rec_sdfnode *sdf = nullptr;
+    const jsrt_rec_sdfgeom *sdfg = nullptr;
+    uint32_t n_mc = 0, n_mat = 0, n_geom = 0, n_obj = 0, n_mats = 0, n_root = 0, n_chld = 0, n_bvh = 0, n_tri = 0,
+             n_lite = 0, n_sdf = 0, n_sdfg = 0;
+};
+
+struct LoadError {
+    std::string msg;
+};
+[[noreturn]] void fail(const std::string &m) { throw LoadError{m}; }
+
+template <class T>
+void bind(const jsrt_section &s, const uint8_t *base, const T *&ptr, uint32_t &n, const char *name) {
+    if (s.bytes != (uint64_t)s.count * sizeof(T)) fail(std::string("bad section size: ") + name);
+    ptr = reinterpret_cast<const T *>(base + s.offset);
+    n = s.count;
+}
+
+Blob parse(const void *data, size_t nbytes) {
+    Blob B;
+    const uint8_t *b = static_cast<const uint8_t *>(data);
+    if (!b || nbytes < sizeof(jsrt_blob_header)) fail("scene blob too small");
+    const auto *h = reinterpret_cast<const jsrt_blob_header *>(b);
+    if (h->magic != JSRT_MAGIC) fail("not a JSRT scene blob");
+    if (h->version != JSRT_VERSION) fail("unsupported JSRT blob version");
+    if (sizeof(*h) + (uint64_t)h->n_sections * sizeof(jsrt_section) > nbytes) fail("truncated section table");
+    const auto *sec = reinterpret_cast<const jsrt_section *>(b + sizeof(*h));
+    for (uint32_t i = 0; i < h->n_sections; ++i) {
+        const jsrt_section &s = sec[i];
+        if (s.offset > nbytes || s.bytes > nbytes - s.offset) fail("section out of range");
+        if (s.offset % 8) fail("misaligned section");
+        uint32_t one = 0;
+        switch (s.tag) {
+        case JSRT_SEC_RENDERER: bind(s, b, B.rndr, one, "RNDR"); if (one != 1) fail("need one renderer"); break;
+        case JSRT_SEC_CAMERA: bind(s, b, B.cam, one, "CAMR"); if (one != 1) fail("need one camera"); break;
+        case JSRT_SEC_MCOLOR: bind(s, b, B.mc, B.n_mc, "MCOL"); break;
+        case JSRT_SEC_MATERIAL: bind(s, b, B.mat, B.n_mat, "MATL"); break;
+        case JSRT_SEC_GEOMETRY: bind(s, b, B.geom, B.n_geom, "GEOM"); break;
+        case JSRT_SEC_OBJECT: bind(s, b, B.obj, B.n_obj, "OBJS"); break;
+        case JSRT_SEC_MATRIX: bind(s, b, B.mats, B.n_mats, "MATS"); break;
+        case JSRT_SEC_ROOT: bind(s, b, B.root, B.n_root, "ROOT"); break;
+        case JSRT_SEC_CHILD: bind(s, b, B.chld, B.n_chld, "CHLD"); break;
+        case JSRT_SEC_BVHNODE: bind(s, b, B.bvh, B.n_bvh, "BVHN"); break;
+        case JSRT_SEC_TRIANGLE: bind(s, b, B.tri, B.n_tri, "TRIS"); break;
+        case JSRT_SEC_LIGHT: bind(s, b, B.lite, B.n_lite, "LITE"); break;
+        case JSRT_SEC_SDFNODE: bind(s, b, B.sdf, B.n_sdf, "SDFN"); break;
+        case JSRT_SEC_SDFGEOM: bind(s, b, B.sdfg, B.n_sdfg, "SDFG"); break;
+        default: break;  // unknown sections are ignored (forward compatible)
+        }
+    }
+    if (!B.rndr || !B.cam) fail("scene blob lacks renderer/camera");
+    return B;
+}
+
+// Row 3 must map w exactly as (0,0,0,1) does after the f32 store: the kernels carry w implicitly
+// (1 for points, 0 for directions).  Mat4.inverse can leave m33 = 0.9999999999999998, whose f32
+// rounding is exactly 1 (tests/AMultipleBVH), so compare in f32 for m33.
+bool is_affine(const double *m) {
+    for (int i = 0; i < 12; ++i)  // a NaN in rows 0..2 makes every transformed ray NaN: no hit,
+        if (m[i] != m[i]) return true;  // whatever row 3 holds (tests/SDF_RecursiveUnionTest: Math.pi)
+    return m[12] == 0 && m[13] == 0 && m[14] == 0 && (float)m[15] == 1.0f;
+}
+bool is_identity(const double *m) {
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (m[4 * r + c] != (r == c ? 1.0 : 0.0)) return false;
+    return true;
+}
+
+// Mat*Mat exactly as math.js:399-409 (sum from 0, left to right, float64)
+void mat_mul(const double *A, const double *B, double *R) {
+    double t[16];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            double s = 0;
+            for (int k = 0; k < 4; ++k) s += A[4 * r + k] * B[4 * k + c];
+            t[4 * r + c] = s;
+        }
+    memcpy(R, t, sizeof t);
+}
+
+struct Loader {
+    const Blob &B;
+    HostScene &S;
+    std::unordered_map<int32_t, int32_t> prim_of_obj;   // OBJS idx -> DPrim idx
+    std::unordered_map<int32_t, int32_t> tri_of_blob;   // TRIS idx -> DTri idx
+    std::unordered_map<int32_t, int32_t> bvh_of_root;   // BVHN root -> DBvhNode root
+    std::unordered_map<int32_t, int32_t> bvh_fast;      // BVHN root -> fast flag
+    std::unordered_map<int32_t, int32_t> sdfg_of_blob;
+    std::unordered_map<int32_t, std::pair<int32_t, int32_t>> sdf_code_of;
+
+    Loader(const Blob &b, HostScene &s) : B(b), S(s) {}
+
+    const jsrt_rec_matrix &matrix(int32_t i) {
+        if (i < 0 || (uint32_t)i >= B.n_mats) fail("matrix index out of range");
+        return B.mats[i];
+    }
+
+    void check_mc(int32_t i, int depth = 0) {
+        if (i < 0) return;
+        if ((uint32_t)i >= B.n_mc) fail("material colour index out of range");
+        if (depth > 8) fail("material colour nesting too deep");
+        const jsrt_rec_mcolor &m = B.mc[i];
+        switch (m.kind) {
+        case JSRT_MC_SOLID:
+            if (m.len != 3) fail("colours must be 3-vectors (Vec.of(r,g,b))");
+            break;
+        case JSRT_MC_SCALED_SCALAR: check_mc(m.a, depth + 1); break;
+        case JSRT_MC_SCALED_VEC:
+            if (m.len < 3) fail("vector colour scale shorter than 3");
+            check_mc(m.a, depth + 1);
+            break;
+        case JSRT_MC_CHECKER: check_mc(m.a, depth + 1); check_mc(m.b, depth + 1); break;
+        default: fail("unsupported material colour kind");
+        }
+    }
+
+    int32_t tri_index(int32_t t) {
+        auto it = tri_of_blob.find(t);
+        if (it != tri_of_blob.end()) return it->second;
+        if (t < 0 || (uint32_t)t >= B.n_tri) fail("triangle index out of range");
+        const jsrt_rec_triangle &R = B.tri[t];
+        DTri d;
+        memset(&d, 0, sizeof d);
+        for (int k = 0; k < 3; ++k) {
+            d.n[k] = R.normal[k];
+            d.p0[k] = R.p[0][k];
+            d.v0[k] = R.v0[k];
+            d.v1[k] = R.v1[k];
+        }
+        if (R.normal[3] != 0.0f) fail("triangle normal must have w = 0");
+        d.delta = R.delta;
+        d.d00 = R.d00;
+        d.d11 = R.d11;
+        d.d01 = R.d01;
+        d.denom = R.denom;
+        d.prim = -1;
+        d.shade = -1;
+        if (R.has_normal || R.has_uv) {
+            DTriShade s;
+            memset(&s, 0, sizeof s);
+            memcpy(s.vn, R.vn, sizeof s.vn);
+            memcpy(s.uv, R.uv, sizeof s.uv);
+            s.has_normal = R.has_normal;
+            s.has_uv = R.has_uv;
+            s.uv_len = R.uv_len;
+            if (R.has_uv && (R.uv_len < 2 || R.uv_len > 4)) fail("bad triangle UV length");
+            d.shade = (int32_t)S.trish.size();
+            S.trish.push_back(s);
+        }
+        int32_t idx = (int32_t)S.tris.size();
+        S.tris.push_back(d);
+        tri_of_blob[t] = idx;
+        S.n_triangles++;
+        return idx;
+    }
+
+    int32_t prim_index(int32_t o) {
+        auto it = prim_of_obj.find(o);
+        if (it != prim_of_obj.end()) return it->second;
+        const jsrt_rec_object &O = B.obj[o];
+        if (O.geometry < 0 || (uint32_t)O.geometry >= B.n_geom) fail("geometry index out of range");
+        if (O.material < 0 || (uint32_t)O.material >= B.n_mat) fail("primitive without material");
+        const jsrt_rec_matrix &M = matrix(O.matrix);
+        if (!is_affine(M.inv)) fail("non-affine primitive transforms are not supported");
+        const jsrt_rec_geometry &G = B.geom[O.geometry];
+        DPrim p;
+        memset(&p, 0, sizeof p);
+        memcpy(p.inv, M.inv, sizeof p.inv);
+        p.gkind = (int32_t)G.kind;
+        p.gindex = -1;
+        p.material = O.material;
+        p.casts_shadow = O.casts_shadow ? 1 : 0;
+        switch (G.kind) {
+        case JSRT_GEOM_PLANE:
+        case JSRT_GEOM_SQUARE:
+        case JSRT_GEOM_CIRCLE:
+        case JSRT_GEOM_SPHERE:
+        case JSRT_GEOM_CYLINDER: break;
+        case JSRT_GEOM_AABB: memcpy(p.center, G.center, 16); memcpy(p.half, G.half, 16); break;
+        case JSRT_GEOM_TRIANGLE: p.gindex = tri_index(G.index); break;
+        case JSRT_GEOM_SDF: p.gindex = sdfg_index(G.index); break;
+        default: fail("unsupported geometry kind");
+        }
+        int32_t idx = (int32_t)S.prims.size();
+        S.prims.push_back(p);
+        prim_of_obj[o] = idx;
+        return idx;
+    }
+
+    // ---- BVH (aggregates.js:187-225) ----
+    int32_t bvh_node(int32_t n, int depth, bool &fast) {
+        if (n < 0 || (uint32_t)n >= B.n_bvh) fail("BVH node index out of range");
+        if (depth > 60) fail("BVH too deep");
+        const jsrt_rec_bvhnode &R = B.bvh[n];
+        int32_t idx = (int32_t)S.bvh.size();
+        S.bvh.push_back(DBvhNode{});
+        S.n_bvh_nodes++;
+        DBvhNode d;
+        d.cx = R.center[0]; d.cy = R.center[1]; d.cz = R.center[2];
+        d.hx = R.half[0]; d.hy = R.half[1]; d.hz = R.half[2];
+        if (R.is_leaf) {
+            d.a = (int32_t)S.leaf_prims.size();
+            d.b = ~R.n_obj;
+            for (int32_t i = 0; i < R.n_obj; ++i) {
+                const int32_t o = B.chld[R.first_obj + i];
+                if (o < 0 || (uint32_t)o >= B.n_obj) fail("BVH leaf object out of range");
+                if (B.obj[o].kind != JSRT_OBJ_PRIMITIVE) fail("BVH leaves must hold Primitives");
+                const int32_t p = prim_index(o);
+                S.leaf_prims.push_back(p);
+                const DPrim &P = S.prims[p];
+                const bool tri = P.gkind == JSRT_GEOM_TRIANGLE;
+                S.leaf_tris.push_back(tri ? P.gindex : -1);
+                const jsrt_rec_matrix &M = matrix(B.obj[o].matrix);
+                if (!(tri && is_identity(M.inv) && P.casts_shadow)) fast = false;
+            }
+        } else {
+            d.a = bvh_node(R.lesser, depth + 1, fast);
+            d.b = bvh_node(R.greater, depth + 1, fast);
+        }
+        S.bvh[idx] = d;
+        return idx;
+    }
+
+    // ---- SDF (sdf.js) -> program (sdf_program.h) ----
+    int32_t kconst(std::initializer_list<double> v) {
+        int32_t i = (int32_t)S.sdf_const.size();
+        for (double x : v) S.sdf_const.push_back(x);
+        return i;
+    }
+    void emit(int32_t op, int32_t a = 0, int32_t b = 0) { S.sdf_insn.push_back(SdfInsn{op, a, b, 0}); }
+    const jsrt_rec_sdfnode &sdfnode(int32_t n) {
+        if (n < 0 || (uint32_t)n >= B.n_sdf) fail("SDF node index out of range");
+        return B.sdf[n];
+    }
+
+    // transformer: multiplies the top of the scale stack by its st (sdf.js:382-477)
+    void compile_transformer(int32_t n, int depth) {
+        if (depth > 32) fail("SDF transformer nesting too deep");
+        const jsrt_rec_sdfnode &N = sdfnode(n);
+        switch (N.kind) {
+        case JSRT_SDFT_SEQUENCE:
+            for (int32_t i = 0; i < N.count; ++i) {
+                emit(SOP_TPUSH);
+                compile_transformer(B.chld[N.first + i], depth + 1);
+                emit(SOP_TPOP_MUL);
+            }
+            break;
+        case JSRT_SDFT_RECURSIVE: {
+            const int32_t loop = (int32_t)S.sdf_insn.size();
+            emit(SOP_LOOP, N.iterations, 0);
+            emit(SOP_TPUSH);
+            compile_transformer(N.a, depth + 1);
+            emit(SOP_TPOP_MUL);
+            S.sdf_insn[loop].b = (int32_t)S.sdf_insn.size();
+            emit(SOP_ENDLOOP, loop);
+            break;
+        }
+        case JSRT_SDFT_MATRIX: {
+            if (!is_affine(N.minv)) fail("non-affine SDF matrix transformer");
+            int32_t c = kconst({N.minv[0], N.minv[1], N.minv[2], N.minv[3], N.minv[4], N.minv[5], N.minv[6],
+                                N.minv[7], N.minv[8], N.minv[9], N.minv[10], N.minv[11]});
+            emit(SOP_XMAT, c, kconst({N.k}));
+            break;
+        }
+        case JSRT_SDFT_REFLECTION:
+            if (N.vec[3] != 0.0f) fail("reflection normal must have w = 0");
+            emit(SOP_XREF, kconst({N.vec[0], N.vec[1], N.vec[2], N.k}));
+            break;
+        case JSRT_SDFT_REPETITION: emit(SOP_XREP, kconst({N.vec[0], N.vec[1], N.vec[2]})); break;
+        default: fail("unsupported SDF transformer");
+        }
+    }
+
+    void compile_sdf(int32_t n, int depth) {
+        if (depth > 32) fail("SDF nesting too deep");
+        const jsrt_rec_sdfnode &N = sdfnode(n);
+        const int32_t start = (int32_t)S.sdf_insn.size();
+        switch (N.kind) {
+        case JSRT_SDF_UNION:
+        case JSRT_SDF_INTERSECTION:
+            if (N.count < 1) fail("empty SDF union/intersection");
+            for (int32_t i = 0; i < N.count; ++i) compile_sdf(B.chld[N.first + i], depth + 1);
+            emit(N.kind == JSRT_SDF_UNION ? SOP_MIN : SOP_MAX, N.count);
+            break;
+        case JSRT_SDF_DIFFERENCE:
+            compile_sdf(N.a, depth + 1);
+            compile_sdf(N.b, depth + 1);
+            emit(SOP_NEG);
+            emit(SOP_MAX, 2);
+            break;
+        case JSRT_SDF_SMOOTH_UNION:
+            compile_sdf(N.a, depth + 1);
+            compile_sdf(N.b, depth + 1);
+            emit(SOP_SMIN, kconst({N.k}));
+            break;
+        case JSRT_SDF_SMOOTH_INTERSECTION:
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_NEG);
+            compile_sdf(N.b, depth + 1);
+            emit(SOP_NEG);
+            emit(SOP_SMIN, kconst({N.k}));
+            emit(SOP_NEG);
+            break;
+        case JSRT_SDF_SMOOTH_DIFFERENCE:
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_NEG);
+            compile_sdf(N.b, depth + 1);
+            emit(SOP_SMIN, kconst({N.k}));
+            emit(SOP_NEG);
+            break;
+        case JSRT_SDF_ROUND:
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_SUBK, kconst({N.k}));
+            break;
+        case JSRT_SDF_SPHERE: emit(SOP_SPHERE, kconst({N.k})); break;
+        case JSRT_SDF_BOX: emit(SOP_BOX, kconst({N.vec[0], N.vec[1], N.vec[2], N.vec[3]})); break;
+        case JSRT_SDF_TETRAHEDRON: emit(SOP_TETRA); break;
+        case JSRT_SDF_TRANSFORM: /* sdf.js:330-333 */
+            emit(SOP_PUSHP);
+            emit(SOP_TPUSH);
+            compile_transformer(N.b, depth + 1);
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_MULS);
+            emit(SOP_TPOP);
+            emit(SOP_POPP);
+            break;
+        case JSRT_SDF_RECURSIVE_UNION: { /* sdf.js:349-357 */
+            emit(SOP_PUSHP);
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_TPUSH);
+            const int32_t loop = (int32_t)S.sdf_insn.size();
+            emit(SOP_LOOP, N.iterations, 0);
+            emit(SOP_TPUSH);
+            compile_transformer(N.b, depth + 1);
+            emit(SOP_TPOP_MUL);
+            compile_sdf(N.a, depth + 1);
+            emit(SOP_MULS);
+            emit(SOP_MIN, 2);
+            S.sdf_insn[loop].b = (int32_t)S.sdf_insn.size();
+            emit(SOP_ENDLOOP, loop);
+            emit(SOP_TPOP);
+            emit(SOP_POPP);
+            break;
+        }
+        default: fail("unsupported SDF node");
+        }
+        if (N.kind == JSRT_SDF_SPHERE || N.kind == JSRT_SDF_BOX || N.kind == JSRT_SDF_TETRAHEDRON)
+            if (N.basecolor_len != 3) fail("SDF basecolor must be a 3-vector");
+        if (!sdf_code_of.count(n)) sdf_code_of[n] = {start, (int32_t)S.sdf_insn.size()};
+    }
+
+    // Static stack-depth check of one compiled program (loops have zero net effect).
+    void check_sdf_stacks(size_t begin, size_t end) {
+        int d = 0, p = 0, sc = 0, l = 0, md = 0, mp = 0, ms = 0, ml = 0;
+        for (size_t i = begin; i < end; ++i) {
+            const SdfInsn &I = S.sdf_insn[i];
+            switch (I.op) {
+            case SOP_BOX: case SOP_SPHERE: case SOP_TETRA: ++d; break;
+            case SOP_MIN: case SOP_MAX: d -= I.a - 1; break;
+            case SOP_SMIN: --d; break;
+            case SOP_PUSHP: ++p; break;
+            case SOP_POPP: --p; break;
+            case SOP_TPUSH: ++sc; break;
+            case SOP_TPOP: case SOP_TPOP_MUL: --sc; break;
+            case SOP_LOOP: ++l; break;
+            case SOP_ENDLOOP: --l; break;
+            default: break;
+            }
+            md = d > md ? d : md; mp = p > mp ? p : mp; ms = sc > ms ? sc : ms; ml = l > ml ? l : ml;
+            if (d < 0 || p < 0 || sc < 0 || l < 0) fail("SDF program stack underflow");
+        }
+        if (md > SDF_MAX_D || mp > SDF_MAX_P || ms > SDF_MAX_S || ml > SDF_MAX_LOOP)
+            fail("SDF tree too deep/wide for the GPU program stacks");
+    }
+
+    int32_t sdfg_index(int32_t g) {
+        auto it = sdfg_of_blob.find(g);
+        if (it != sdfg_of_blob.end()) return it->second;
+        if (g < 0 || (uint32_t)g >= B.n_sdfg) fail("SDF geometry index out of range");
+        jsrt_rec_sdfgeom G = B.sdfg[g];
+        const size_t first = S.sdf_insn.size();
+        compile_sdf(G.root, 0);
+        emit(SOP_END);
+        check_sdf_stacks(first, S.sdf_insn.size());
+        int32_t idx = (int32_t)S.sdfg.size();
+        S.sdfg.push_back(G);
+        sdfg_of_blob[g] = idx;
+        return idx;
+    }
+
+    // ---- object graph -> instance tree ----
+    int32_t inst(int32_t o, const double *ctx_mat, int depth) {
+        if (o < 0 || (uint32_t)o >= B.n_obj) fail("object index out of range");
+        if (depth > 8) fail("aggregate nesting deeper than 8 levels");
+        const jsrt_rec_object &O = B.obj[o];
+        DInst d;
+        memset(&d, 0, sizeof d);
+        d.kind = 0;
+        switch (O.kind) {
+        case JSRT_OBJ_PRIMITIVE:
+            d.kind = INST_PRIM;
+            d.prim = prim_index(o);
+            break;
+        case JSRT_OBJ_AGGREGATE:
+        case JSRT_OBJ_BVH: {
+            const jsrt_rec_matrix &M = matrix(O.matrix);
+            if (!is_affine(M.inv)) fail("non-affine aggregate transforms are not supported");
+            d.matrix = (int32_t)(S.mats.size() / 12);
+            for (int k = 0; k < 12; ++k) S.mats.push_back(M.inv[k]);
+            double child_ctx[16];
+            mat_mul(M.inv, ctx_mat, child_ctx);  // world.js:37-39
+            d.ctx = (int32_t)(S.ctx.size() / 16);
+            for (int k = 0; k < 16; ++k) S.ctx.push_back(child_ctx[k]);
+            if (O.kind == JSRT_OBJ_BVH) {
+                d.kind = INST_BVH;
+                auto it = bvh_of_root.find(O.bvh_root);
+                if (it == bvh_of_root.end()) {
+                    bool fast = true;
+                    const int32_t r = bvh_node(O.bvh_root, 0, fast);
+                    bvh_of_root[O.bvh_root] = r;
+                    bvh_fast[O.bvh_root] = fast ? 1 : 0;
+                    it = bvh_of_root.find(O.bvh_root);
+                }
+                d.first = it->second;
+                d.count = bvh_fast[O.bvh_root];
+            } else {
+                d.kind = INST_AGG;
+                std::vector<int32_t> kids;
+                for (int32_t i = 0; i < O.n_children; ++i) kids.push_back(inst(B.chld[O.first_child + i], child_ctx, depth + 1));
+                d.first = (int32_t)S.inst_child.size();
+                d.count = (int32_t)kids.size();
+                for (int32_t k : kids) S.inst_child.push_back(k);
+            }
+            break;
+        }
+        default: fail("unsupported world object (TransformedWorldObject is not renderable in the reference either)");
+        }
+        int32_t idx = (int32_t)S.insts.size();
+        S.insts.push_back(d);
+        return idx;
+    }
+
+    // Area light world normal: inv_transform.transposed().times(n).to4(0).normalized() (lights.js:90)
+    void area_normal(const double *Ti, float *out) {
+        const double n[4] = {0, 0, 1, 0};
+        float r[4];
+        for (int i = 0; i < 4; ++i) {  // transposed row i = column i of Ti; dot over the 4-vector n
+            double s = n[0] * Ti[0 * 4 + i] + n[1] * Ti[1 * 4 + i] + n[2] * Ti[2 * 4 + i] + n[3] * Ti[3 * 4 + i];
+            r[i] = (float)s;
+        }
+        auto or0 = [](float x) { return (x != x || x == 0.0f) ? 0.0f : x; };
+        float v[4] = {r[0], or0(r[1]), or0(r[2]), 0.0f};
+        double nn = sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3]);
+        if (nn > 0.00001) {
+            const double s = 1 / nn;
+            for (int i = 0; i < 4; ++i) v[i] = (float)((double)v[i] * s);
+        }
+        memcpy(out, v, sizeof v);
+    }
+
+    void run() {
+        const jsrt_rec_renderer &R = *B.rndr;
+        S.kind = (int32_t)R.kind;
+        S.spp = (int32_t)R.spp;
+        S.max_depth = (int32_t)R.max_depth;
+        S.width = (int32_t)R.width;
+        S.height = (int32_t)R.height;
+        if (R.bg_len != 3) fail("World.bg_color must be a 3-vector");
+        memcpy(S.bg, R.bg, sizeof S.bg);
+        const jsrt_rec_camera &C = *B.cam;
+        if (!is_affine(C.transform)) fail("non-affine camera transform");
+        memcpy(S.cam.T, C.transform, sizeof S.cam.T);
+        S.cam.tan_fov = C.tan_fov;
+        S.cam.aspect = C.aspect;
+        S.cam.focus = C.focus_distance;
+        S.cam.sensor = C.sensor_size;
+        S.cam.kind = (int32_t)C.kind;
+
+        for (uint32_t i = 0; i < B.n_mat; ++i) {
+            const jsrt_rec_material &M = B.mat[i];
+            if (M.kind < JSRT_MAT_PHONG || M.kind > JSRT_MAT_TRANSPARENT) fail("unsupported material kind");
+            if (M.kind == JSRT_MAT_SOLID || M.kind == JSRT_MAT_TRANSPARENT) check_mc(M.color);
+            else {
+                check_mc(M.ambient); check_mc(M.diffuse); check_mc(M.specular); check_mc(M.reflect); check_mc(M.transmit);
+                if (M.ambient < 0 || M.diffuse < 0 || M.specular < 0 || M.reflect < 0 || M.transmit < 0)
+                    fail("Phong material lacks a colour");
+                if (M.kind == JSRT_MAT_PATH && !isfinite(M.smoothness))
+                    fail("infinite-smoothness path-tracing scatter is broken in the reference (materials.js:430)");
+            }
+            S.mat.push_back(M);
+        }
+        for (uint32_t i = 0; i < B.n_mc; ++i) S.mc.push_back(B.mc[i]);
+
+        const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        for (int k = 0; k < 16; ++k) S.ctx.push_back(I[k]);  // ctx 0: World.color's Mat4.identity()
+        S.all_roots_prims = 1;
+        for (uint32_t i = 0; i < B.n_root; ++i) {
+            const int32_t ix = inst(B.root[i], I, 0);
+            S.roots.push_back(ix);
+            if (S.insts[ix].kind != INST_PRIM) S.all_roots_prims = 0;
+        }
+        for (uint32_t i = 0; i < B.n_lite; ++i) {
+            const jsrt_rec_light &L = B.lite[i];
+            DLight d;
+            memset(&d, 0, sizeof d);
+            d.kind = (int32_t)L.kind;
+            d.color = L.color;
+            check_mc(L.color);
+            for (int32_t m = L.color, g = 0; m >= 0 && g < 16; ++g) {  // checkerboard anywhere in the chain?
+                const jsrt_rec_mcolor &mc = B.mc[m];
+                if (mc.kind == JSRT_MC_CHECKER) { d.needs_uv = 1; break; }
+                m = (mc.kind == JSRT_MC_SCALED_SCALAR || mc.kind == JSRT_MC_SCALED_VEC) ? mc.a : -1;
+            }
+            d.gkind = (int32_t)L.geometry_kind;
+            d.samples = (int32_t)L.samples;
+            d.pos_len = (int32_t)L.pos_len;
+            memcpy(d.pos, L.position, sizeof d.pos);
+            memcpy(d.T, L.transform, sizeof d.T);
+            memcpy(d.Ti, L.inv, sizeof d.Ti);
+            if (L.kind == JSRT_LIGHT_POINT) {
+                if (L.pos_len < 3 || L.pos_len > 4) fail("point light position must be a 3- or 4-vector");
+                if (L.pos_len == 4 && L.position[3] != 1.0f) fail("point light position must have w = 1");
+            } else if (L.kind == JSRT_LIGHT_AREA) {
+                if (!is_affine(L.transform) || !is_affine(L.inv)) fail("non-affine area light transform");
+                if (L.geometry_kind != JSRT_GEOM_SQUARE && L.geometry_kind != JSRT_GEOM_CIRCLE &&
+                    L.geometry_kind != JSRT_GEOM_SPHERE)
+                    fail("unsupported area light surface");
+                area_normal(L.inv, d.wn);
+            } else fail("unsupported light kind");
+            S.lights.push_back(d);
+        }
+        for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);
+        if (B.n_sdf) S.sdf_child.assign(B.chld, B.chld + B.n_chld);
+        S.sdf_range.assign(2 * (size_t)B.n_sdf, -1);
+        for (auto &kv : sdf_code_of) {
+            S.sdf_range[2 * kv.first] = kv.second.first;
+            S.sdf_range[2 * kv.first + 1] = kv.second.second;
+        }
+    }
+};
+
+}  // namespace
+
+int load_scene(const void *blob, size_t nbytes, HostScene &out, std::string &err) {
+    try {
+        Blob B = parse(blob, nbytes);
+        out = HostScene();
+        Loader L(B, out);
+        L.run();
+        return 0;
+    } catch (const LoadError &e) {
+        err = e.msg;
+        return -1;
+    } catch (const std::exception &e) {
+        err = std::string("scene load: ") + e.what();
+        return -1;
+    }
+}
+
+}  // namespace jsrt

@@ -1,0 +1,41 @@
+// scene_load.h — host side: JSRT blob -> validated, flattened HostScene (then uploaded to HBM).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "device_scene.h"
+
+namespace jsrt {
+
+struct HostScene {
+    std::vector<DPrim> prims;
+    std::vector<DInst> insts;
+    std::vector<int32_t> inst_child, roots;
+    std::vector<double> mats, ctx;
+    std::vector<DBvhNode> bvh;
+    std::vector<int32_t> leaf_prims, leaf_tris;
+    std::vector<DTri> tris;
+    std::vector<DTriShade> trish;
+    std::vector<jsrt_rec_material> mat;
+    std::vector<jsrt_rec_mcolor> mc;
+    std::vector<DLight> lights;
+    std::vector<SdfInsn> sdf_insn;
+    std::vector<double> sdf_const;
+    std::vector<int32_t> sdf_range;
+    std::vector<int32_t> sdf_child;
+    std::vector<jsrt_rec_sdfnode> sdf_nodes;
+    std::vector<jsrt_rec_sdfgeom> sdfg;
+    DCamera cam;
+    float bg[4];
+    int32_t kind, spp, max_depth, width, height;
+    int32_t all_roots_prims;
+    // workload facts used for algorithmic-byte accounting
+    int64_t n_bvh_nodes = 0, n_triangles = 0;
+};
+
+// Returns 0 on success; otherwise fills err.
+int load_scene(const void *blob, size_t nbytes, HostScene &out, std::string &err);
+
+}  // namespace jsrt

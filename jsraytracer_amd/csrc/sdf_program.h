@@ -1,0 +1,49 @@
+// sdf_program.h — SDF trees (sdf.js:53-477) compiled to a small stack program.
+//
+// The reference evaluates SDFs by recursive virtual calls (SDF.distance / SDFTransformer.transform).
+// On the GPU every lane of a wave marches the same SDF, so the tree is compiled once at scene load
+// into a linear program whose instruction stream is wave-uniform; per-lane state is the current
+// point P (f32 xyz, w == 1 everywhere on this path), a float64 distance stack and a float64 scale
+// stack that reproduces the reference's nesting of `s = s * st` products exactly.
+//
+// Each SDF node compiles to a contiguous range [start, end) that pushes exactly one distance and
+// leaves P unchanged, so getMaterialData (sdf.js:87,103,120,...) can evaluate any child by range.
+#pragma once
+#include <stdint.h>
+
+namespace jsrt {
+
+enum SdfOp : int32_t {
+    SOP_END = 0,
+    SOP_BOX,        // a = const index of size (4 doubles: f32 size xyz, as double)   sdf.js:276-279
+    SOP_SPHERE,     // a = const index of radius                                       sdf.js:232-234
+    SOP_TETRA,      //                                                                 sdf.js:305-308
+    SOP_MIN,        // a = n: pop n, push Math.min(...)                                sdf.js:83-85
+    SOP_MAX,        // a = n: pop n, push Math.max(...)                                sdf.js:99-101
+    SOP_NEG,        // d = -d
+    SOP_SUBK,       // a = const: d = d - k                                            sdf.js:210-212
+    SOP_SMIN,       // a = const k: pop b, pop a, push smoothMin(a, b, k)              sdf.js:128-131
+    SOP_PUSHP,      // save P
+    SOP_POPP,       // restore P
+    SOP_TPUSH,      // push scale 1
+    SOP_TPOP,       // drop scale
+    SOP_TPOP_MUL,   // st = pop; top = top * st
+    SOP_MULS,       // d = d * top-scale
+    SOP_XMAT,       // a = const index of 12 doubles (inv rows 0..2), b = const of scale:
+                    //   P = inv*P, top = top * scale                                   sdf.js:433-435
+    SOP_XREF,       // a = const: normal xyz (f32 as double) + delta                    sdf.js:450-455
+    SOP_XREP,       // a = const: sizes xyz                                             sdf.js:471-473
+    SOP_LOOP,       // a = iterations, b = index of the matching SOP_ENDLOOP
+    SOP_ENDLOOP,    // a = index of the matching SOP_LOOP
+};
+
+struct SdfInsn {
+    int32_t op, a, b, pad;
+};
+
+constexpr int SDF_MAX_D = 16;   // distance stack depth
+constexpr int SDF_MAX_P = 8;    // point stack depth
+constexpr int SDF_MAX_S = 8;    // scale stack depth
+constexpr int SDF_MAX_LOOP = 4; // nested loops
+
+}  // namespace jsrt

@@ -1,0 +1,156 @@
+"""Host-side mirror of the reference's renderer interface, backed by the HIP library.
+
+Reference: src/renderers.js (SimpleRenderer.render :10-41, IncrementalMultisamplingRenderer.render
+:70-117), src/pixelbuffer.js (PixelBuffer :1-50), src/worker.js (:17-40).  Same names, argument
+meaning and error behaviour: ``render(img, timelimit=0, callback=False, x_offset=0, x_delt=1)``
+fills ``img``'s RGBA8 bytes for the columns px = x_offset, x_offset + x_delt, ... and calls
+``callback({"pass": p, "completion": c})`` no more often than every ``timelimit`` ms.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import JsrtError, Params, Stats, check
+
+RENDERER_KINDS = {"SimpleRenderer": 0, "IncrementalMultisamplingRenderer": 1, "RandomMultisamplingRenderer": 2}
+
+
+class PixelBuffer:
+    """pixelbuffer.js:1-50 — RGBA8 image (ImageData-like) with the reference's setColor rules."""
+
+    def __init__(self, width, height=None):
+        if isinstance(width, np.ndarray):
+            self.imgdata = width
+        else:
+            self.imgdata = np.zeros((height, width, 4), np.uint8)  # new ImageData: zero-filled
+
+    def width(self):
+        return self.imgdata.shape[1]
+
+    def height(self):
+        return self.imgdata.shape[0]
+
+    def coord(self, x, y):
+        return y * (self.width() * 4) + x * 4
+
+    def getColor(self, x, y):
+        return self.imgdata[y, x].astype(np.float64) / 255
+
+
+class Scene:
+    """A JSRT scene blob (include/jsrt_scene.h) uploaded to one HIP device."""
+
+    def __init__(self, blob, device=0):
+        L = _native.lib()
+        if L.jsrt_device_count() <= 0:
+            raise JsrtError("no HIP device visible: the MI355X renderer has no CPU fallback")
+        self._blob = bytes(blob)
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(self._blob, len(self._blob))
+        check(L.jsrt_scene_create(buf, len(self._blob), device, ctypes.byref(h)), "jsrt_scene_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _native.lib().jsrt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def params(width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, device=0,
+               samples_per_launch=0, timelimit_ms=0.0):
+        return Params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, device, samples_per_launch,
+                      timelimit_ms)
+
+    def render(self, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1,
+               samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0):
+        """Render into host arrays.  Returns (rgba u8[H,W,4], colors f32[H,W,4] or None, stats)."""
+        L = _native.lib()
+        p = self.params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, self.device,
+                        samples_per_launch, timelimit_ms)
+        W = width if width > 0 else self.header()["width"]
+        H = height if height > 0 else self.header()["height"]
+        if rgba is None:
+            rgba = np.zeros((H, W, 4), np.uint8)
+        assert rgba.shape == (H, W, 4) and rgba.dtype == np.uint8 and rgba.flags.c_contiguous
+        colors = np.full((H, W, 4), np.nan, np.float32) if want_colors else None
+        st = Stats()
+        cb = PROGRESS_NONE
+        if progress is not None:
+            cb = _native.PROGRESS_FN(lambda ps, c, u: progress(int(ps), float(c)))
+        rc = L.jsrt_render(self._h, ctypes.byref(p), rgba.ctypes.data,
+                           colors.ctypes.data if colors is not None else None, cb, None, ctypes.byref(st))
+        check(rc, "jsrt_render")
+        return rgba, colors, st.as_dict()
+
+    def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, **kw):
+        """Render owned columns into device buffers (see jsrt.h jsrt_render_device)."""
+        L = _native.lib()
+        p = self.params(device=self.device, **kw)
+        st = Stats()
+        rc = L.jsrt_render_device(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
+                                  ctypes.byref(st))
+        check(rc, "jsrt_render_device")
+        return st.as_dict()
+
+    def header(self):
+        return scene_header(self._blob)
+
+
+PROGRESS_NONE = ctypes.cast(None, _native.PROGRESS_FN)
+
+
+def owned_columns(width, x_offset, x_delt, col_block=1):
+    return int(_native.lib().jsrt_owned_columns(width, x_offset, x_delt, col_block))
+
+
+def scene_header(blob):
+    import struct
+    magic, version, nsec, _ = struct.unpack_from("<4I", blob, 0)
+    if magic != 0x5452534A or version != 1:
+        raise JsrtError("not a JSRT v1 scene blob")
+    for i in range(nsec):
+        tag, count, off, nbytes = struct.unpack_from("<IIQQ", blob, 16 + 24 * i)
+        if tag == 0x52444E52:  # 'RNDR'
+            kind, spp, depth, w, h = struct.unpack_from("<5I", blob, off)
+            return {"kind": kind, "spp": spp, "max_depth": depth, "width": w, "height": h}
+    raise JsrtError("scene blob has no renderer record")
+
+
+class HipRenderer:
+    """Drop-in for SimpleRenderer / IncrementalMultisamplingRenderer / RandomMultisamplingRenderer
+    (renderers.js).  ``scene`` is a Scene (or blob); kind/spp/depth default to the blob's renderer."""
+
+    def __init__(self, scene, samplesPerPixel=None, maxRecursionDepth=None, kind=None, seed=1, device=0):
+        self.scene = scene if isinstance(scene, Scene) else Scene(scene, device)
+        hdr = self.scene.header()
+        self.kind = hdr["kind"] if kind is None else (RENDERER_KINDS[kind] if isinstance(kind, str) else kind)
+        self.samplesPerPixel = hdr["spp"] if samplesPerPixel is None else samplesPerPixel
+        self.maxRecursionDepth = hdr["max_depth"] if maxRecursionDepth is None else maxRecursionDepth
+        self.seed = seed
+
+    @staticmethod
+    def computePixelCount(img, x_offset, x_delt):  # renderers.js:7-9
+        return ((img.width() / x_delt) + round(1 - x_offset / x_delt) * (img.width() % x_delt)) * img.height()
+
+    def render(self, img, timelimit=0, callback=False, x_offset=0, x_delt=1):
+        if x_delt <= 0:
+            raise JsrtError("x_delt must be positive")
+        progress = None
+        spl = 0
+        if timelimit and callback:
+            spl = max(1, self.samplesPerPixel // 8)  # progressive launches so the cadence is observable
+
+            def progress(p, c):
+                callback({"pass": p, "completion": c})
+        self.scene.render(img.width(), img.height(), self.samplesPerPixel, self.maxRecursionDepth, self.kind,
+                          self.seed, x_offset, x_delt, samples_per_launch=spl, rgba=img.imgdata, want_colors=False,
+                          progress=progress, timelimit_ms=float(timelimit or 0))
+        return img

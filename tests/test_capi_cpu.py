@@ -1,0 +1,70 @@
+"""CPU-side checks of the drop-in boundary (no GPU needed): the C-ABI library loads and exports
+every symbol include/jsrt.h declares, the blob exporter/format round-trips, and host helpers behave."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from jsraytracer_amd import build as jb
+    jb.build()
+    from jsraytracer_amd import _native
+    return _native.lib()
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    return sorted(set(re.findall(r"\b(jsrt_[a-z_]+)\s*\(", txt)) - {"jsrt_progress_fn"})
+
+
+def test_header_symbols_exported(lib):
+    from jsraytracer_amd import _native
+    declared = _declared("jsrt.h")
+    assert set(declared) == set(_native.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in declared:
+        assert re.search(rf"\bT {sym}$", out, re.M), f"{sym} not exported"
+        assert hasattr(lib, sym)
+
+
+def test_library_is_gfx950(lib):
+    from jsraytracer_amd import _native
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+                          f"--input={_native.LIB_PATH}"], capture_output=True, text=True)
+    listing = out.stdout + out.stderr
+    if out.returncode != 0 or not listing.strip():  # fall back to scanning the embedded code object
+        listing = open(_native.LIB_PATH, "rb").read().decode("latin-1")
+    assert "gfx950" in listing
+
+
+def test_abi_version_and_helpers(lib):
+    assert lib.jsrt_abi_version() == 1
+    from jsraytracer_amd import owned_columns
+    assert owned_columns(10, 0, 1) == 10
+    assert owned_columns(10, 1, 3) == 3            # 1, 4, 7
+    assert owned_columns(10, 3, 3) == 3            # 3, 6, 9 (reference allows offset >= delt)
+    assert owned_columns(40, 1, 2, 8) == 16        # blocks 1 and 3 of 8 columns
+    assert owned_columns(36, 1, 2, 8) == 16        # blocks 1 (8..15) and 3 (24..31)
+    assert owned_columns(36, 0, 2, 8) == 20        # blocks 0, 2 and the partial block 4 (32..35)
+
+
+def test_no_device_raises_not_falls_back(lib):
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    if lib.jsrt_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(jr.JsrtError):
+        jr.Scene(pyoracle.golden_scene("ASimpleScene"))
+
+
+def test_scene_header_reader():
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    h = jr.scene_header(pyoracle.golden_scene("cornell_box_path"))
+    assert h == {"kind": 1, "spp": 128, "max_depth": 8, "width": 600, "height": 600}
