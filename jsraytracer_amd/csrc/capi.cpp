@@ -90,7 +90,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     sc->device = device;
     DeviceArena A;
     const size_t o_prims = A.add(H.prims), o_insts = A.add(H.insts), o_ichild = A.add(H.inst_child),
-                 o_roots = A.add(H.roots), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
+                 o_roots = A.add(H.roots), o_rb = A.add(H.rbounds), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
                  o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
                  o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
@@ -105,6 +105,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.insts = (const DInst *)(b + o_insts);
     D.inst_child = (const int32_t *)(b + o_ichild);
     D.roots = (const int32_t *)(b + o_roots);
+    D.rbounds = (const RootBound *)(b + o_rb);
     D.mats = (const double *)(b + o_mats);
     D.ctx = (const double *)(b + o_ctx);
     D.bvh = (const DBvhNode *)(b + o_bvh);
@@ -128,6 +129,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.cam = H.cam;
     memcpy(D.bg, H.bg, sizeof D.bg);
     D.all_roots_prims = H.all_roots_prims;
+    D.profile = H.profile;
     *out = sc.release();
     return 0;
 }

@@ -19,6 +19,12 @@ namespace jsrt {
 
 enum : int32_t { INST_PRIM = 1, INST_AGG = 2, INST_BVH = 3 };
 
+// Kernel profiles: the render kernel is instantiated per feature set so that a scene without
+// BVHs / aggregates / SDFs / triangles does not pay their register footprint.
+enum : int32_t { PF_BVH = 1, PF_AGG = 2, PF_SDF = 4, PF_TRI = 8 };
+enum : int32_t { PF_ANALYTIC = 0, PF_MESH = PF_BVH | PF_TRI, PF_SDF_ONLY = PF_SDF, PF_ALL = 15 };
+#define PF_SDF_PROFILE PF_SDF
+
 struct DPrim {           // world.js:104 Primitive
     double inv[12];      // inv_transform rows 0..2 (row 3 verified == 0,0,0,1 at load)
     int32_t gkind;       // JSRT_GEOM_*
@@ -40,6 +46,16 @@ struct DInst {           // one node of the object tree flattened per path (shar
     int32_t ctx;         // AGG/BVH: shading context id of everything below it
     int32_t pad[2];
 };
+
+struct RootBound {       // conservative world-space box of one top-level object (culling only)
+    float lo[3];
+    float k;             // margin per unit of |ray origin|_inf
+    float hi[3];
+    float e0;            // constant margin
+    int32_t bounded;     // 0: unbounded (Plane, ...) -> never culled
+    int32_t pad[3];
+};
+static_assert(sizeof(RootBound) == 48, "RootBound");
 
 struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
     float cx, cy, cz;
@@ -86,6 +102,7 @@ struct DScene {
     const DInst *insts;
     const int32_t *inst_child;
     const int32_t *roots;
+    const RootBound *rbounds;   // parallel to roots
     const double *mats;      // 12 doubles per AGG/BVH instance matrix
     const double *ctx;       // 16 doubles per shading context (ctx 0 = identity)
     const DBvhNode *bvh;
@@ -106,7 +123,8 @@ struct DScene {
     DCamera cam;
     float bg[4];
     int32_t all_roots_prims; // every root is an INST_PRIM (uniform fast path)
-    int32_t pad[3];
+    int32_t profile;         // PF_* feature set the kernel is instantiated for
+    int32_t pad[2];
 };
 
 }  // namespace jsrt

@@ -24,6 +24,9 @@ namespace jsrt {
 
 #define JS_PI 3.141592653589793
 #define DINF __builtin_inf()
+#ifndef JSRT_WAVES_PER_SIMD
+#define JSRT_WAVES_PER_SIMD 2
+#endif
 
 // --------------------------------------------------------------------------------------------
 // JS scalar semantics
@@ -485,6 +488,7 @@ struct Hit {
     int ctx;
 };
 
+template <int PF>
 __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DPrim &P, F3 o, F3 d, double minD,
                                                        double maxD) {
     switch (P.gkind) {
@@ -513,22 +517,27 @@ __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DP
             return (tmin >= minD) ? tmin : tmax;
         return -DINF;
     }
-    case JSRT_GEOM_TRIANGLE: return tri_intersect(S.tris[P.gindex], o, d);
-    case JSRT_GEOM_SDF: return sdf_intersect(S, P.gindex, o, d, minD, maxD);
+    case JSRT_GEOM_TRIANGLE:
+        if (PF & PF_TRI) return tri_intersect(S.tris[P.gindex], o, d);
+        return -DINF;
+    case JSRT_GEOM_SDF:
+        if (PF & PF_SDF) return sdf_intersect(S, P.gindex, o, d, minD, maxD);
+        return -DINF;
     default: return -DINF;
     }
 }
 
 // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
+template <int PF>
 __device__ __forceinline__ double prim_intersect(const DScene &S, int pi, F3 o, F3 d, double minD, double maxD,
                                                  bool transp) {
     const DPrim &P = S.prims[pi];
     if (!transp && !P.casts_shadow) return DINF;
-    return prim_intersect_local(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
+    return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
 }
 
 // BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
-template <bool ANY>
+template <int PF, bool ANY>
 __device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, I.ctx};
     const bool fast = I.count != 0;
@@ -545,7 +554,7 @@ __device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD
                 for (int k = 0; k < cnt; ++k) {
                     double t;
                     if (fast) t = tri_intersect(S.tris[S.leaf_tris[N.a + k]], o, d);
-                    else t = prim_intersect(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp);
+                    else t = prim_intersect<PF>(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp);
                     if (t > minD && t < maxD && t < best.t) {
                         best.t = t;
                         best.prim = S.leaf_prims[N.a + k];
@@ -563,7 +572,7 @@ __device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD
 
 // Aggregate / BVH instance below the top level (aggregates.js:14-18): members flattened in DFS
 // order into the caller's running closest hit (equivalent to nested first-minimum selection).
-template <bool ANY>
+template <int PF, bool ANY>
 __device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, double maxD, bool transp, Hit &best) {
     struct Fr {
         int inst, next;
@@ -579,7 +588,7 @@ __device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, 
         Fr &f = st[sp - 1];
         const DInst &I = S.insts[f.inst];
         if (I.kind == INST_BVH) {
-            const Hit h = bvh_cast<ANY>(S, I, f.o, f.d, minD, maxD, transp);
+            const Hit h = bvh_cast<PF, ANY>(S, I, f.o, f.d, minD, maxD, transp);
             --sp;
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
@@ -591,7 +600,7 @@ __device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, 
         const int c = S.inst_child[I.first + f.next++];
         const DInst &C = S.insts[c];
         if (C.kind == INST_PRIM) {
-            const double t = prim_intersect(S, C.prim, f.o, f.d, minD, maxD, transp);
+            const double t = prim_intersect<PF>(S, C.prim, f.o, f.d, minD, maxD, transp);
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, C.prim, I.ctx};
                 if (ANY) return;
@@ -605,29 +614,60 @@ __device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, 
 }
 
 // World.cast (world.js:28-30); ANY = shadow query (only `0 < d < 1` of the closest is read,
-// materials.js:250-252, so the first accepted hit decides)
-template <bool ANY>
+// materials.js:250-252, so the first accepted hit decides).
+//
+// Culling: every top-level object carries a world-space box inflated by a margin
+// >= 1e3 x the f32 rounding bound of any point the exact test can accept.  A lane skips an object
+// when its ray segment (minD, min(best, maxD)) provably misses that box, and the wave skips the
+// object when no lane needs it.  Skipped objects could not have produced an accepted hit, so the
+// closest hit (first minimum in World.objects order) is unchanged bit for bit.
+template <int PF, bool ANY>
 __device__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, 0};
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
+    const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    const float fminD = (float)minD;
+    bool live = true;
     for (int i = 0; i < S.n_roots; ++i) {
+        const RootBound &RB = S.rbounds[i];
+        bool need = live;
+        if (RB.bounded) {
+            const float e = RB.k * oabs + RB.e0;
+            float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
+            float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
+            a0 = (RB.lo[1] - e - o.y) * iy;
+            a1 = (RB.hi[1] + e - o.y) * iy;
+            tn = fmaxf(tn, fminf(a0, a1));
+            tf = fminf(tf, fmaxf(a0, a1));
+            a0 = (RB.lo[2] - e - o.z) * iz;
+            a1 = (RB.hi[2] + e - o.z) * iz;
+            tn = fmaxf(tn, fminf(a0, a1));
+            tf = fminf(tf, fmaxf(a0, a1));
+            const float lim = (float)(best.t < maxD ? best.t : maxD);
+            need = need && (tn <= tf) && (tf >= fminD) && (tn <= lim);
+        }
+        if (!__any(need)) continue;
+        if (!need) continue;
         const int ri = S.roots[i];
         const DInst &I = S.insts[ri];
         if (I.kind == INST_PRIM) {
-            const double t = prim_intersect(S, I.prim, o, d, minD, maxD, transp);
+            const double t = prim_intersect<PF>(S, I.prim, o, d, minD, maxD, transp);
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, I.prim, 0};
-                if (ANY) return best;
+                if (ANY) live = false;
             }
-        } else if (I.kind == INST_BVH) {
+        } else if (!(PF & (PF_BVH | PF_AGG))) {
+            continue;
+        } else if ((PF & PF_BVH) && I.kind == INST_BVH) {
             const double *m = S.mats + 12 * I.matrix;
-            const Hit h = bvh_cast<ANY>(S, I, xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
+            const Hit h = bvh_cast<PF, ANY>(S, I, xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
-                if (ANY) return best;
+                if (ANY) live = false;
             }
-        } else {
-            nested_cast<ANY>(S, ri, o, d, minD, maxD, transp, best);
-            if (ANY && best.prim >= 0) return best;
+        } else if (PF & PF_AGG) {
+            nested_cast<PF, ANY>(S, ri, o, d, minD, maxD, transp, best);
+            if (ANY && best.prim >= 0) live = false;
         }
     }
     return best;
@@ -702,6 +742,7 @@ __device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, 
 }
 
 // PhongMaterial.colorFromLights (materials.js:240-259) with lights.js sampleIterators
+template <int PF>
 __device__ F3 color_from_lights(const DScene &S, int mkind, const ShadeData &d, Rng &rng) {
     F3 ret = d.ambient;
     for (int li = 0; li < S.n_lights; ++li) {
@@ -754,8 +795,10 @@ __device__ F3 color_from_lights(const DScene &S, int mkind, const ShadeData &d, 
                 lcol = scale(mc_eval(S, Lt.color, u, v), sc);
             }
             // shadow test (materials.js:250-252)
-            const Hit sh = world_cast<true>(S, d.pos, delta, 0.0001, 1, false);
+#ifndef JSRT_DIAG_NO_SHADOW
+            const Hit sh = world_cast<PF, true>(S, d.pos, delta, 0.0001, 1, false);
             if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) continue;
+#endif
             light_color = add(light_color, light_sample_color(mkind, d, delta, lcol));
         }
         if (ns > 0) ret = add(ret, scale(light_color, 1.0 / ns));
@@ -790,6 +833,7 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
 
 // World.color hit branch: Primitive.color (world.js:125-137) + Geometry.materialData + Material.color.
 // Returns the number of children (0..2) written to `fr` (fr.surface always set).
+template <int PF>
 __device__ int shade(const DScene &S, const Hit &h, F3 o, F3 d, int depth_in, uint32_t addr, uint32_t pixkey,
                      Frame &fr) {
     const DPrim &P = S.prims[h.prim];
@@ -855,6 +899,7 @@ __device__ int shade(const DScene &S, const Hit &h, F3 o, F3 d, int depth_in, ui
         break;
     }
     case JSRT_GEOM_TRIANGLE: {  // geometry.js:376-409
+        if (!(PF & PF_TRI)) break;
         const DTri &T = S.tris[P.gindex];
         nrm = f3(T.n[0], T.n[1], T.n[2]);
         if (T.shade >= 0) {
@@ -877,6 +922,7 @@ __device__ int shade(const DScene &S, const Hit &h, F3 o, F3 d, int depth_in, ui
         break;
     }
     case JSRT_GEOM_SDF: {  // SDFGeometry.materialData (sdf.js:41-47)
+        if (!(PF & PF_SDF)) break;
         const jsrt_rec_sdfgeom &G = S.sdfg[P.gindex];
         const double dist0 = sdf_node_dist(S, G.root, pl);
         const float step = (float)G.normal_step;
@@ -965,7 +1011,11 @@ __device__ int shade(const DScene &S, const Hit &h, F3 o, F3 d, int depth_in, ui
             sd.refr = add(scale(neg(sd.V), r), scale(Nn, r * vdotn - sqrt(k)));
         }
     }
-    fr.surface = color_from_lights(S, mkind, sd, rng);
+#ifdef JSRT_DIAG_NO_LIGHTS
+    fr.surface = sd.ambient;
+#else
+    fr.surface = color_from_lights<PF>(S, mkind, sd, rng);
+#endif
     int n = 0;
     if (mkind == JSRT_MAT_PHONG) {  // materials.js:277-288
         if (dot3(sd.refl, sd.refl) > 0) fr.c[n++] = Child{sd.R, f3(1, 1, 1), sd.refl, 1.0};
@@ -1028,7 +1078,8 @@ __device__ __forceinline__ uint32_t set_color_rgba(F3 c) {  // PixelBuffer.setCo
 }
 
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void render_kernel(DScene S, RenderArgs A) {
+template <int PF>
+__global__ __launch_bounds__(256, JSRT_WAVES_PER_SIMD) void render_kernel(DScene S, RenderArgs A) {
     const int wave = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
     if (wave >= A.patches) return;
@@ -1082,13 +1133,13 @@ __global__ __launch_bounds__(256) void render_kernel(DScene S, RenderArgs A) {
             color = f3(0, 0, 0);
             returned = true;
         } else {
-            const Hit h = world_cast<false>(S, ro, rd, minD, DINF, true);
+            const Hit h = world_cast<PF, false>(S, ro, rd, minD, DINF, true);
             if (h.prim < 0) {
                 color = f3(S.bg[0], S.bg[1], S.bg[2]);
                 returned = true;
             } else {
                 Frame &f = stk[sp];
-                const int n = shade(S, h, ro, rd, depth - 1, addr, pixkey, f);
+                const int n = shade<PF>(S, h, ro, rd, depth - 1, addr, pixkey, f);
                 if (n == 0) {
                     color = f.surface;
                     returned = true;
@@ -1158,7 +1209,12 @@ __global__ __launch_bounds__(256) void render_kernel(DScene S, RenderArgs A) {
 hipError_t launch_render(const DScene &scene, const RenderArgs &args, hipStream_t stream) {
     const int blocks = (args.patches + 3) / 4;
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(render_kernel, dim3(blocks), dim3(256), 0, stream, scene, args);
+    switch (scene.profile) {
+    case PF_ANALYTIC: hipLaunchKernelGGL(render_kernel<PF_ANALYTIC>, dim3(blocks), dim3(256), 0, stream, scene, args); break;
+    case PF_MESH: hipLaunchKernelGGL(render_kernel<PF_MESH>, dim3(blocks), dim3(256), 0, stream, scene, args); break;
+    case PF_SDF: hipLaunchKernelGGL(render_kernel<PF_SDF>, dim3(blocks), dim3(256), 0, stream, scene, args); break;
+    default: hipLaunchKernelGGL(render_kernel<PF_ALL>, dim3(blocks), dim3(256), 0, stream, scene, args); break;
+    }
     return hipGetLastError();
 }
 

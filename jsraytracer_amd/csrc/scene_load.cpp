@@ -105,6 +105,68 @@ void mat_mul(const double *A, const double *B, double *R) {
     memcpy(R, t, sizeof t);
 }
 
+// ---- conservative world bounds for culling (never change results: DESIGN.md §3.4) ----
+struct LBox {
+    double lo[3], hi[3];
+    bool bounded;
+};
+
+// General 4x4 inverse (Gauss-Jordan, partial pivoting, long double): maps local -> world.
+bool invert4(const double *m, long double *out) {
+    long double a[4][8];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 8; ++c) a[r][c] = c < 4 ? (long double)m[4 * r + c] : (c - 4 == r ? 1.0L : 0.0L);
+    for (int c = 0; c < 4; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < 4; ++r)
+            if (fabsl(a[r][c]) > fabsl(a[piv][c])) piv = r;
+        if (!(fabsl(a[piv][c]) > 0) || !isfinite((double)a[piv][c])) return false;
+        if (piv != c)
+            for (int k = 0; k < 8; ++k) { long double t = a[c][k]; a[c][k] = a[piv][k]; a[piv][k] = t; }
+        const long double d = a[c][c];
+        for (int k = 0; k < 8; ++k) a[c][k] /= d;
+        for (int r = 0; r < 4; ++r)
+            if (r != c) {
+                const long double f = a[r][c];
+                for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+            }
+    }
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) out[4 * r + c] = a[r][4 + c];
+    return true;
+}
+
+double frob3(const long double *m) {  // Frobenius norm of the linear 3x3 part
+    long double s = 0;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) s += m[4 * r + c] * m[4 * r + c];
+    return (double)sqrtl(s);
+}
+
+// Box in the parent space of an object whose world->local matrix is `inv`; kappa accumulates the
+// condition number of the linear part (error amplification).
+LBox to_parent(const LBox &b, const double *inv, double &kappa) {
+    LBox r;
+    r.bounded = false;
+    if (!b.bounded) return r;
+    long double T[16], M[16];
+    if (!invert4(inv, T)) return r;
+    for (int i = 0; i < 16; ++i) M[i] = inv[i];
+    kappa *= frob3(M) * frob3(T);
+    for (int k = 0; k < 3; ++k) { r.lo[k] = INFINITY; r.hi[k] = -INFINITY; }
+    for (int c = 0; c < 8; ++c) {
+        const long double p[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+        for (int k = 0; k < 3; ++k) {
+            const long double v = T[4 * k] * p[0] + T[4 * k + 1] * p[1] + T[4 * k + 2] * p[2] + T[4 * k + 3];
+            r.lo[k] = fmin(r.lo[k], (double)v);
+            r.hi[k] = fmax(r.hi[k], (double)v);
+        }
+    }
+    r.bounded = true;
+    for (int k = 0; k < 3; ++k) r.bounded &= isfinite(r.lo[k]) && isfinite(r.hi[k]);
+    return r;
+}
+
 struct Loader {
     const Blob &B;
     HostScene &S;
@@ -114,6 +176,9 @@ struct Loader {
     std::unordered_map<int32_t, int32_t> bvh_fast;      // BVHN root -> fast flag
     std::unordered_map<int32_t, int32_t> sdfg_of_blob;
     std::unordered_map<int32_t, std::pair<int32_t, int32_t>> sdf_code_of;
+    std::vector<LBox> prim_box;                          // local bound per DPrim
+    double cur_leaf_kappa = 1;
+    std::unordered_map<int32_t, double> bvh_leaf_kappa;  // BVHN root -> max leaf condition number
 
     Loader(const Blob &b, HostScene &s) : B(b), S(s) {}
 
@@ -211,6 +276,40 @@ struct Loader {
         int32_t idx = (int32_t)S.prims.size();
         S.prims.push_back(p);
         prim_of_obj[o] = idx;
+        LBox lb;
+        lb.bounded = true;
+        auto set = [&](double x0, double y0, double z0, double x1, double y1, double z1) {
+            lb.lo[0] = x0; lb.lo[1] = y0; lb.lo[2] = z0; lb.hi[0] = x1; lb.hi[1] = y1; lb.hi[2] = z1;
+        };
+        switch (G.kind) {
+        case JSRT_GEOM_SQUARE: set(-0.5, -0.5, 0, 0.5, 0.5, 0); break;
+        case JSRT_GEOM_CIRCLE: set(-1, -1, 0, 1, 1, 0); break;
+        case JSRT_GEOM_SPHERE:
+        case JSRT_GEOM_CYLINDER: set(-1, -1, -1, 1, 1, 1); break;
+        case JSRT_GEOM_AABB:
+            set((double)G.center[0] - G.half[0], (double)G.center[1] - G.half[1], (double)G.center[2] - G.half[2],
+                (double)G.center[0] + G.half[0], (double)G.center[1] + G.half[1], (double)G.center[2] + G.half[2]);
+            break;
+        case JSRT_GEOM_TRIANGLE: {
+            const jsrt_rec_triangle &T = B.tri[G.index];
+            set(INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            for (int v = 0; v < 3; ++v)
+                for (int k = 0; k < 3; ++k) {
+                    lb.lo[k] = fmin(lb.lo[k], (double)T.p[v][k]);
+                    lb.hi[k] = fmax(lb.hi[k], (double)T.p[v][k]);
+                }
+            break;
+        }
+        case JSRT_GEOM_SDF: {
+            const jsrt_rec_sdfgeom &SG = B.sdfg[G.index];
+            set((double)SG.center[0] - SG.half[0], (double)SG.center[1] - SG.half[1], (double)SG.center[2] - SG.half[2],
+                (double)SG.center[0] + SG.half[0], (double)SG.center[1] + SG.half[1], (double)SG.center[2] + SG.half[2]);
+            break;
+        }
+        default: lb.bounded = false; break;  // SimplePlane / Plane: unbounded
+        }
+        for (int k = 0; k < 3; ++k) lb.bounded &= isfinite(lb.lo[k]) && isfinite(lb.hi[k]);
+        prim_box.push_back(lb);
         return idx;
     }
 
@@ -239,6 +338,11 @@ struct Loader {
                 S.leaf_tris.push_back(tri ? P.gindex : -1);
                 const jsrt_rec_matrix &M = matrix(B.obj[o].matrix);
                 if (!(tri && is_identity(M.inv) && P.casts_shadow)) fast = false;
+                if (!is_identity(M.inv)) {
+                    double kk = 1;
+                    LBox lb = to_parent(prim_box[p], M.inv, kk);
+                    cur_leaf_kappa = fmax(cur_leaf_kappa, lb.bounded ? kk : INFINITY);
+                }
             }
         } else {
             d.a = bvh_node(R.lesser, depth + 1, fast);
@@ -443,7 +547,9 @@ struct Loader {
                 auto it = bvh_of_root.find(O.bvh_root);
                 if (it == bvh_of_root.end()) {
                     bool fast = true;
+                    cur_leaf_kappa = 1;
                     const int32_t r = bvh_node(O.bvh_root, 0, fast);
+                    bvh_leaf_kappa[O.bvh_root] = cur_leaf_kappa;
                     bvh_of_root[O.bvh_root] = r;
                     bvh_fast[O.bvh_root] = fast ? 1 : 0;
                     it = bvh_of_root.find(O.bvh_root);
@@ -465,6 +571,70 @@ struct Loader {
         int32_t idx = (int32_t)S.insts.size();
         S.insts.push_back(d);
         return idx;
+    }
+
+    // Bound of instance `i` in its parent's space; kappa = error amplification below the parent.
+    LBox inst_bound(int32_t i, double &kappa) {
+        const DInst &I = S.insts[i];
+        if (I.kind == INST_PRIM) {
+            double m[16];
+            for (int k = 0; k < 12; ++k) m[k] = S.prims[I.prim].inv[k];
+            m[12] = m[13] = m[14] = 0; m[15] = 1;
+            return to_parent(prim_box[I.prim], m, kappa);
+        }
+        LBox local;
+        local.bounded = true;
+        double kin = 1;
+        if (I.kind == INST_BVH) {
+            const DBvhNode &R = S.bvh[I.first];
+            local.lo[0] = (double)R.cx - R.hx; local.lo[1] = (double)R.cy - R.hy; local.lo[2] = (double)R.cz - R.hz;
+            local.hi[0] = (double)R.cx + R.hx; local.hi[1] = (double)R.cy + R.hy; local.hi[2] = (double)R.cz + R.hz;
+            for (auto &kv : bvh_of_root)
+                if (kv.second == I.first) kin = bvh_leaf_kappa[kv.first];
+        } else {
+            for (int k = 0; k < 3; ++k) { local.lo[k] = INFINITY; local.hi[k] = -INFINITY; }
+            for (int32_t c = 0; c < I.count; ++c) {
+                double kc = 1;
+                const LBox cb = inst_bound(S.inst_child[I.first + c], kc);
+                if (!cb.bounded) { local.bounded = false; break; }
+                kin = fmax(kin, kc);
+                for (int k = 0; k < 3; ++k) { local.lo[k] = fmin(local.lo[k], cb.lo[k]); local.hi[k] = fmax(local.hi[k], cb.hi[k]); }
+            }
+        }
+        for (int k = 0; k < 3; ++k) local.bounded &= isfinite(local.lo[k]) && isfinite(local.hi[k]);
+        double m[16];
+        for (int k = 0; k < 12; ++k) m[k] = S.mats[12 * I.matrix + k];
+        m[12] = m[13] = m[14] = 0; m[15] = 1;
+        kappa *= kin;
+        return to_parent(local, m, kappa);
+    }
+
+    void root_bounds() {
+        for (int32_t r : S.roots) {
+            RootBound rb;
+            memset(&rb, 0, sizeof rb);
+            double kappa = 1;
+            const LBox b = inst_bound(r, kappa);
+            rb.bounded = b.bounded && isfinite(kappa) && kappa < 1e6;
+            if (rb.bounded) {
+                double c2 = 0, r2 = 0;
+                for (int k = 0; k < 3; ++k) {
+                    const double c = 0.5 * (b.lo[k] + b.hi[k]), h = 0.5 * (b.hi[k] - b.lo[k]);
+                    c2 += c * c;
+                    r2 += h * h;
+                }
+                // margin >= 1e3 x the f32 rounding bound 4u*kappa*(|o| + |c| + R) of an accepted hit point
+                const double k = 1e-4 * kappa * sqrt(3.0);
+                const double e0 = 1e-4 * kappa * (sqrt(c2) + sqrt(r2)) + 1e-6 * (1 + sqrt(r2));
+                rb.k = (float)(k * 1.001);
+                rb.e0 = (float)(e0 * 1.001);
+                for (int i = 0; i < 3; ++i) {
+                    rb.lo[i] = nextafterf((float)b.lo[i], -INFINITY);
+                    rb.hi[i] = nextafterf((float)b.hi[i], INFINITY);
+                }
+            }
+            S.rbounds.push_back(rb);
+        }
     }
 
     // Area light world normal: inv_transform.transposed().times(n).to4(0).normalized() (lights.js:90)
@@ -526,6 +696,7 @@ struct Loader {
             S.roots.push_back(ix);
             if (S.insts[ix].kind != INST_PRIM) S.all_roots_prims = 0;
         }
+        root_bounds();
         for (uint32_t i = 0; i < B.n_lite; ++i) {
             const jsrt_rec_light &L = B.lite[i];
             DLight d;
@@ -556,6 +727,17 @@ struct Loader {
             } else fail("unsupported light kind");
             S.lights.push_back(d);
         }
+        int32_t f = 0;
+        for (const DInst &in : S.insts) {
+            if (in.kind == INST_BVH) f |= PF_BVH | PF_TRI;
+            if (in.kind == INST_AGG) f |= PF_AGG;
+        }
+        for (const DPrim &pr : S.prims) {
+            if (pr.gkind == JSRT_GEOM_SDF) f |= PF_SDF;
+            if (pr.gkind == JSRT_GEOM_TRIANGLE) f |= PF_TRI;
+        }
+        S.features = f;
+        S.profile = f == 0 ? PF_ANALYTIC : (f & ~PF_MESH) == 0 ? PF_MESH : (f & ~PF_SDF) == 0 ? PF_SDF : PF_ALL;
         for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);
         if (B.n_sdf) S.sdf_child.assign(B.chld, B.chld + B.n_chld);
         S.sdf_range.assign(2 * (size_t)B.n_sdf, -1);

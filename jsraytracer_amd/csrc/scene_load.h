@@ -13,6 +13,7 @@ struct HostScene {
     std::vector<DPrim> prims;
     std::vector<DInst> insts;
     std::vector<int32_t> inst_child, roots;
+    std::vector<RootBound> rbounds;
     std::vector<double> mats, ctx;
     std::vector<DBvhNode> bvh;
     std::vector<int32_t> leaf_prims, leaf_tris;
@@ -31,6 +32,7 @@ struct HostScene {
     float bg[4];
     int32_t kind, spp, max_depth, width, height;
     int32_t all_roots_prims;
+    int32_t features = 0, profile = PF_ALL;  // PF_* bits used / kernel instantiation chosen
     // workload facts used for algorithmic-byte accounting
     int64_t n_bvh_nodes = 0, n_triangles = 0;
 };
