@@ -136,6 +136,8 @@ def main():
     elapsed = float(tt.item())
 
     kernel_ms = sum(s["kernel_ms"] for s in stats) / len(stats)
+    stage_ms = {k: sum(s["stage_ms"][k] for s in stats) / len(stats) for k in stats[0]["stage_ms"]}
+    stage_launches = stats[0]["stage_launches"]
     kt = torch.tensor([kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
     if world > 1:
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
@@ -166,6 +168,8 @@ def main():
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"tiles{world}",
                        "col_block": cb},
             "roofline": roof, "cpu_baseline": cpu,
+            "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
+            "stage_launches_per_step": stage_launches,
         }
         print(json.dumps(line))
     if world > 1:

@@ -40,18 +40,21 @@ typedef struct {
     uint32_t seed;           /* keyed RNG seed (DESIGN.md "keyed RNG") */
     int32_t x_offset, x_delt;/* reference column partition (renderers.js:21,88); x_delt <= 0 -> 1 */
     int32_t device;          /* HIP device ordinal */
-    int32_t samples_per_launch; /* progressive chunking: samples per pixel per kernel launch (<=0: all) */
+    int32_t samples_per_launch; /* progress granularity: samples per pixel between callbacks (<=0: all) */
     double timelimit_ms;     /* progress callback cadence (renderers.js:28-37); 0 = no callback */
-    int32_t reserved[6];
+    int32_t max_paths;       /* wavefront batch size in paths (<= 0: library default) */
+    int32_t reserved[5];
 } jsrt_params;
 
+#define JSRT_STAGES 8
 typedef struct {
-    double kernel_ms;        /* sum of render-kernel durations (HIP events on the render stream) */
+    double kernel_ms;        /* sum of all render-kernel durations (HIP events on the render stream) */
     double total_ms;         /* host wall time of the call */
     uint64_t samples;        /* pixel-samples rendered */
     uint32_t launches;       /* render-kernel launches */
-    uint32_t reserved0;
-    double reserved[4];
+    uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
+    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final */
+    uint32_t stage_launches[JSRT_STAGES];
 } jsrt_stats;
 
 typedef void (*jsrt_progress_fn)(int32_t pass, double completion, void *user);

@@ -20,16 +20,22 @@ class Params(ctypes.Structure):
                 ("max_depth", ctypes.c_int32), ("kind", ctypes.c_int32), ("seed", ctypes.c_uint32),
                 ("x_offset", ctypes.c_int32), ("x_delt", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("samples_per_launch", ctypes.c_int32), ("timelimit_ms", ctypes.c_double),
-                ("reserved", ctypes.c_int32 * 6)]
+                ("max_paths", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
+
+
+STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "unused"]
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("samples", ctypes.c_uint64),
-                ("launches", ctypes.c_uint32), ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_double * 4)]
+                ("launches", ctypes.c_uint32), ("batches", ctypes.c_uint32), ("stage_ms", ctypes.c_double * 8),
+                ("stage_launches", ctypes.c_uint32 * 8)]
 
     def as_dict(self):
         return {"kernel_ms": self.kernel_ms, "total_ms": self.total_ms, "samples": int(self.samples),
-                "launches": int(self.launches)}
+                "launches": int(self.launches), "batches": int(self.batches),
+                "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(7)},
+                "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(7)}}
 
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)

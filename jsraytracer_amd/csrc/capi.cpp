@@ -6,6 +6,9 @@
 #include <string.h>
 
 #include <chrono>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -46,6 +49,9 @@ struct jsrt_scene {
     void *dmem = nullptr;
     DScene ds;
     HostScene hs;
+    int ns = 0;            // light samples per lit node
+    std::mutex wf_mutex;   // guards the cached wavefront buffers
+    Wavefront wf;
 };
 
 extern "C" {
@@ -130,6 +136,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     memcpy(D.bg, H.bg, sizeof D.bg);
     D.all_roots_prims = H.all_roots_prims;
     D.profile = H.profile;
+    for (const DLight &L : H.lights) sc->ns += L.kind == JSRT_LIGHT_POINT ? 1 : L.samples;
     *out = sc.release();
     return 0;
 }
@@ -181,52 +188,59 @@ int resolve(const jsrt_scene *s, const jsrt_params *p, int32_t col_block, Resolv
     return 0;
 }
 
-// Runs the launch sequence (chunked by samples_per_launch) on `stream`, timing every launch with
-// HIP events recorded on that stream.
+// Renders one frame (all spp) on `stream` through the wavefront schedule (render.hip); every
+// kernel launch is bracketed by HIP events recorded on that same stream.
 int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_rgba, float *d_colors,
                  hipStream_t stream, jsrt_progress_fn progress, void *user, jsrt_stats *st) {
-    const int per = (p && p->samples_per_launch > 0) ? p->samples_per_launch : a.spp;
-    const int nl = (a.spp + per - 1) / per;
+    const size_t nacc = (size_t)a.ncols * a.H * 4;
     float *accum = nullptr;
-    if (nl > 1) HIP_TRY(hipMallocAsync((void **)&accum, (size_t)a.ncols * a.H * 4 * sizeof(float), stream));
-    std::vector<hipEvent_t> ev(2 * (size_t)nl);
-    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipMallocAsync((void **)&accum, nacc * sizeof(float) + 16, stream));
     a.rgba = d_rgba;
     a.colors = d_colors;
     a.accum = accum;
+    a.final_pass = 1;
+    std::unique_lock<std::mutex> lk(s->wf_mutex, std::try_to_lock);  // re-entrant: busy cache -> own buffers
+    std::unique_ptr<Wavefront> own;
+    Wavefront *wf = &s->wf;
+    if (!lk.owns_lock()) {
+        own.reset(new Wavefront());
+        wf = own.get();
+    }
+    KernelTimes kt;
     auto t_last = std::chrono::steady_clock::now();
     const double tl = p ? p->timelimit_ms : 0;
-    int rc = 0;
-    for (int l = 0; l < nl && !rc; ++l) {
-        a.s_begin = l * per;
-        a.s_end = std::min(a.spp, a.s_begin + per);
-        a.final_pass = (l == nl - 1);
-        if (hipEventRecord(ev[2 * l], stream) != hipSuccess) rc = set_error(-3, "hipEventRecord");
-        hipError_t e = launch_render(s->ds, a, stream);
-        if (e != hipSuccess) { rc = set_error(-3, std::string("render launch: ") + hipGetErrorString(e)); break; }
-        if (hipEventRecord(ev[2 * l + 1], stream) != hipSuccess) rc = set_error(-3, "hipEventRecord");
-        if (progress && tl > 0 && l + 1 < nl) {  // renderers.js:103-112 cadence, at launch granularity
-            if (hipStreamSynchronize(stream) != hipSuccess) { rc = set_error(-3, "render failed"); break; }
+    std::function<bool(int, double)> prog;
+    if (progress && tl > 0)
+        prog = [&](int pass, double completion) {  // renderers.js:103-112 cadence, at batch granularity
+            if (completion >= 1.0) return true;
             auto now = std::chrono::steady_clock::now();
             if (std::chrono::duration<double, std::milli>(now - t_last).count() >= tl) {
                 t_last = now;
-                progress(a.s_end - 1, (double)a.s_end / a.spp, user);
+                progress(pass, completion, user);
             }
-        }
-    }
+            return true;
+        };
+    size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : (size_t)2 << 20;
+    if (const char *e = getenv("JSRT_MAX_PATHS")) max_paths = (size_t)atoll(e);
+    hipError_t e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
+    int rc = 0;
+    if (e != hipSuccess) rc = set_error(-3, std::string("render: ") + hipGetErrorString(e));
     if (!rc && st) {
-        if (hipStreamSynchronize(stream) != hipSuccess) rc = set_error(-3, "render kernel failed");
+        if (hipStreamSynchronize(stream) != hipSuccess) rc = set_error(-3, "render kernels failed");
         double ms = 0;
-        for (int l = 0; l < nl && !rc; ++l) {
-            float x = 0;
-            if (hipEventElapsedTime(&x, ev[2 * l], ev[2 * l + 1]) == hipSuccess) ms += x;
+        uint32_t launches = 0;
+        for (int k = 0; k < KT_N && k < JSRT_STAGES; ++k) {
+            st->stage_ms[k] = kt.ev[k].total_ms();
+            st->stage_launches[k] = (uint32_t)kt.ev[k].used;
+            ms += st->stage_ms[k];
+            launches += (uint32_t)kt.ev[k].used;
         }
         st->kernel_ms = ms;
-        st->launches = (uint32_t)nl;
+        st->launches = launches;
+        st->batches = (uint32_t)kt.ev[KT_ACCUM].used;
         st->samples = (uint64_t)a.ncols * a.H * a.spp;
     }
-    if (accum) (void)hipFreeAsync(accum, stream);
-    for (auto &e : ev) (void)hipEventDestroy(e);
+    (void)hipFreeAsync(accum, stream);
     return rc;
 }
 

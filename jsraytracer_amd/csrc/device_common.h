@@ -1,0 +1,835 @@
+// device_common.h — device-side building blocks shared by the render kernels: the reference's
+// scalar semantics (Math.max/min/pow/round, toPrecision(8) fmod), the keyed RNG, f32-stored Vec
+// arithmetic, ray transforms, geometry intersections, the SDF program VM, world casts with
+// conservative culling, material colours and light-sample / scatter math.
+//
+// Numerics follow the reference's model: Vec components are float32 after every
+// Vec op; scalars are float64; each binary op is one IEEE op (built with -ffp-contract=off).
+// f32 (+,-,*,/) of two f32 operands is done natively in f32 (bit-identical to f64-then-round);
+// f32 * f64 scalar is done in f64 then rounded.  Random numbers come from the keyed,
+// ray-tree-addressed generator, identical to oracle/refharness/keyed_rng.js.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_scene.h"
+
+namespace jsrt {
+
+#define JS_PI 3.141592653589793
+#define DINF __builtin_inf()
+
+// --------------------------------------------------------------------------------------------
+// JS scalar semantics
+__device__ __forceinline__ bool is_nan(double x) { return x != x; }
+__device__ __forceinline__ double js_max(double a, double b) {  // Math.max
+    if (is_nan(a) || is_nan(b)) return __builtin_nan("");
+    if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) && __builtin_signbit(b)) ? -0.0 : 0.0;
+    return a > b ? a : b;
+}
+__device__ __forceinline__ double js_min(double a, double b) {  // Math.min
+    if (is_nan(a) || is_nan(b)) return __builtin_nan("");
+    if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) || __builtin_signbit(b)) ? -0.0 : 0.0;
+    return a < b ? a : b;
+}
+__device__ __forceinline__ double js_sign(double x) {
+    if (is_nan(x) || x == 0.0) return x;
+    return x > 0 ? 1.0 : -1.0;
+}
+__device__ __forceinline__ double js_pow(double x, double y) {
+    if (is_nan(y)) return __builtin_nan("");
+    if (y == 0.0) return 1.0;
+    if ((x == 1.0 || x == -1.0) && __builtin_isinf(y)) return __builtin_nan("");
+    return pow(x, y);
+}
+__device__ __forceinline__ double js_round(double x) {  // Math.round (half toward +inf)
+    if (!__builtin_isfinite(x) || x == 0.0) return x;
+    double r = floor(x);
+    if (x - r >= 0.5) r += 1.0;
+    return r;
+}
+__device__ __forceinline__ float or0(float x) { return (x != x || x == 0.0f) ? 0.0f : x; }  // `x || 0`
+
+// Number(v.toPrecision(8)) — ECMA-262 toPrecision (ties -> larger n) then correctly rounded parse.
+// Exact for 1e-12 <= |v| < 2^64 (128-bit products, no 128-bit division); outside that window the
+// 8-digit rounding is applied in float64 (documented in DESIGN.md; no reference scene reaches it).
+__device__ double to_precision8(double v) {
+    if (!__builtin_isfinite(v)) return v;
+    if (v == 0.0) return 0.0;
+    const bool neg = v < 0;
+    const double x = fabs(v);
+    int ex;
+    const double f = frexp(x, &ex);
+    const uint64_t M = (uint64_t)ldexp(f, 53);
+    const int E = ex - 53;
+    int e10 = (int)floor(log10(x));
+    uint64_t n = 0;
+    const uint64_t P10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                              100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull,
+                              10000000000000ull, 100000000000000ull, 1000000000000000ull, 10000000000000000ull,
+                              100000000000000000ull, 1000000000000000000ull, 10000000000000000000ull};
+    bool ok = false;
+    for (int it = 0; it < 4; ++it) {
+        const int k = 7 - e10;
+        uint64_t q;
+        bool up;
+        if (k >= 0) {
+            if (k > 19 || E >= 0) break;
+            const unsigned __int128 num = (unsigned __int128)M * P10[k];
+            const int s = -E;
+            if (s >= 127) break;
+            const unsigned __int128 qq = num >> s;
+            const unsigned __int128 rem = num - (qq << s);
+            if (qq >= (unsigned __int128)1000000000ull) { e10 += 1; continue; }
+            q = (uint64_t)qq;
+            up = (rem << 1) >= ((unsigned __int128)1 << s);
+        } else {
+            const int m = -k;
+            if (m > 19 || ex > 64) break;
+            uint64_t num, den;
+            if (E >= 0) { num = M << E; den = P10[m]; }
+            else {
+                num = M;
+                if (-E > 63 || P10[m] > (~0ull >> -E)) break;
+                den = P10[m] << -E;
+            }
+            q = num / den;
+            const uint64_t rem = num - q * den;
+            up = rem >= den - rem;  // 2*rem >= den without overflow
+        }
+        if (q < 10000000ull) { e10 -= 1; continue; }
+        if (q >= 100000000ull) { e10 += 1; continue; }
+        n = q + (up ? 1 : 0);
+        if (n == 100000000ull) { n = 10000000ull; e10 += 1; }
+        ok = true;
+        break;
+    }
+    double r;
+    if (!ok) {  // outside the exact window
+        const double sc = pow(10.0, (double)(7 - e10));
+        r = floor(x * sc + 0.5) / sc;
+    } else {
+        const int k2 = e10 - 7;
+        const double P10D[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        if (k2 >= 0 && k2 <= 22) r = (double)n * P10D[k2];
+        else if (k2 < 0 && -k2 <= 22) r = (double)n / P10D[-k2];
+        else r = (double)n * pow(10.0, (double)k2);
+    }
+    return neg ? -r : r;
+}
+__device__ __forceinline__ double js_fmod(double a, double b) {  // math.js:27
+    return to_precision8(a - (floor(a / b) * b));
+}
+
+// --------------------------------------------------------------------------------------------
+// keyed RNG (oracle/refharness/keyed_rng.js)
+__device__ __forceinline__ uint32_t mix32(uint32_t h, uint32_t v) {
+    h = (h ^ v) * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    return h;
+}
+// pixkey = mix(mix(seed, pixel), sample), hoisted per sample
+__device__ __forceinline__ double keyed_uniform(uint32_t pixkey, uint32_t node, uint32_t call) {
+    const uint32_t h = mix32(mix32(pixkey, node), call);
+    const uint64_t hi = mix32(h, 0xA5A5A5A5u) >> 5;
+    const uint64_t lo = mix32(h, 0x5A5A5A5Au) >> 6;
+    return (double)(hi * 67108864ull + lo) * (1.0 / 9007199254740992.0);
+}
+struct Rng {
+    uint32_t key, node, calls;
+    __device__ __forceinline__ double next() { return keyed_uniform(key, node, calls++); }
+};
+
+// --------------------------------------------------------------------------------------------
+// 3-component Vec with an implicit w (1 for points, 0 for directions; colours are 3-vectors)
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3 mul(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ F3 scale(F3 a, double s) {  // Vec.times(scalar): f32(x * s) in f64
+    return f3((float)((double)a.x * s), (float)((double)a.y * s), (float)((double)a.z * s));
+}
+__device__ __forceinline__ F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }  // times(-1) is exact
+__device__ __forceinline__ double dot3(F3 a, F3 b) {
+    return (double)a.x * (double)b.x + (double)a.y * (double)b.y + (double)a.z * (double)b.z;
+}
+// normalized() of a Vec whose 4th component is (+/-)0 or absent: the 4th term only adds a zero
+__device__ __forceinline__ F3 normalized(F3 a) {
+    const double n = sqrt(dot3(a, a));
+    return (n > 0.00001) ? scale(a, 1 / n) : a;
+}
+__device__ __forceinline__ double average3(F3 a) {  // Vec.average (math.js:261-266)
+    return ((((0.0 + (double)a.x) + (double)a.y) + (double)a.z)) / 3;
+}
+
+// Mat(3x4 rows, implicit row 3 = 0,0,0,1) * Vec (math.js:392-397): f64 dot in order, f32 store.
+__device__ __forceinline__ F3 xf_point(const double *m, F3 o) {  // w = 1
+    return f3((float)((((double)o.x * m[0] + (double)o.y * m[1]) + (double)o.z * m[2]) + m[3]),
+              (float)((((double)o.x * m[4] + (double)o.y * m[5]) + (double)o.z * m[6]) + m[7]),
+              (float)((((double)o.x * m[8] + (double)o.y * m[9]) + (double)o.z * m[10]) + m[11]));
+}
+__device__ __forceinline__ F3 xf_dir(const double *m, F3 d) {  // w = 0: the 4th term only adds a zero
+    return f3((float)(((double)d.x * m[0] + (double)d.y * m[1]) + (double)d.z * m[2]),
+              (float)(((double)d.x * m[4] + (double)d.y * m[5]) + (double)d.z * m[6]),
+              (float)(((double)d.x * m[8] + (double)d.y * m[9]) + (double)d.z * m[10]));
+}
+// Ray.getPoint (math.js:297-299): origin.plus(direction.times(t))
+__device__ __forceinline__ F3 ray_point(F3 o, F3 d, double t) {
+    return f3(o.x + (float)((double)d.x * t), o.y + (float)((double)d.y * t), o.z + (float)((double)d.z * t));
+}
+// Vec.cartesianToSpherical (math.js:189-193)
+__device__ __forceinline__ void cart_to_sph(F3 n, float &u, float &v) {
+    u = (float)(0.5 + atan2((double)n.z, (double)n.x) / (2 * JS_PI));
+    v = (float)(0.5 - asin((double)n.y) / JS_PI);
+}
+
+// --------------------------------------------------------------------------------------------
+// geometry (geometry.js), local space
+__device__ __forceinline__ bool aabb_slab(float cx, float cy, float cz, float hx, float hy, float hz, F3 o, F3 d,
+                                          double minD, double maxD, double &tmin, double &tmax) {
+    // AABB.get_intersects (geometry.js:189-209)
+    double t_min = -DINF, t_max = DINF;
+    const float p[3] = {cx - o.x, cy - o.y, cz - o.z};
+    const float h[3] = {hx, hy, hz};
+    const float dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double di = (double)dd[i];
+        if (fabs(di) > 0.0000001) {
+            double t1 = ((double)p[i] + (double)h[i]) / di, t2 = ((double)p[i] - (double)h[i]) / di;
+            if (t1 > t2) { const double tmp = t1; t1 = t2; t2 = tmp; }
+            if (t1 > t_min) t_min = t1;
+            if (t2 < t_max) t_max = t2;
+            if (t_min > t_max || t_max < minD || t_min > maxD) return false;
+        } else if (fabs((double)p[i]) > (double)h[i])
+            return false;
+    }
+    tmin = t_min;
+    tmax = t_max;
+    return true;
+}
+
+__device__ __forceinline__ double plane_t(F3 o, F3 d) {  // geometry.js:246-248
+    return (d.z != 0.0f) ? -(double)o.z / (double)d.z : -DINF;
+}
+
+__device__ __forceinline__ double sphere_static(F3 o, F3 d, double minD) {  // geometry.js:429-442
+    const double a = dot3(d, d), b = dot3(d, o), c = dot3(o, o) - 1;
+    double big = b * b - a * c;
+    if (big < 0 || a == 0) return -DINF;
+    big = sqrt(big);
+    const double t1 = (-b + big) / a, t2 = (-b - big) / a;
+    if (t1 >= minD && t2 >= minD) return js_min(t1, t2);
+    return (t2 < minD) ? t1 : t2;
+}
+
+__device__ __forceinline__ double tri_intersect(const DTri &T, F3 o, F3 d) {  // geometry.js:368-375
+    const F3 n = f3(T.n[0], T.n[1], T.n[2]);
+    const double denom = dot3(n, d);
+    const double distance = (denom != 0) ? (T.delta - dot3(n, o)) / denom : -DINF;
+    if (!__builtin_isfinite(distance) || distance < 0) return distance;
+    const F3 p = ray_point(o, d, distance);
+    const F3 v2 = f3(p.x - T.p0[0], p.y - T.p0[1], p.z - T.p0[2]);
+    const double d20 = dot3(v2, f3(T.v0[0], T.v0[1], T.v0[2])), d21 = dot3(v2, f3(T.v1[0], T.v1[1], T.v1[2]));
+    const double v = (T.d11 * d20 - T.d01 * d21) / T.denom, w = (T.d00 * d21 - T.d01 * d20) / T.denom;
+    const float b0 = (float)(1 - v - w), b1 = (float)v, b2 = (float)w;
+    return (b0 >= 0 && b0 <= 1 && b1 >= 0 && b1 <= 1 && b2 >= 0 && b2 <= 1) ? distance : -DINF;
+}
+
+// --------------------------------------------------------------------------------------------
+// SDF program VM (sdf_program.h).  P is the 4-vector point with w == 1.
+__device__ double sdf_run(const DScene &S, int pc, int end, F3 P) {
+    double dst[SDF_MAX_D];
+    F3 pst[SDF_MAX_P];
+    double sst[SDF_MAX_S];
+    int lc[SDF_MAX_LOOP];
+    int dsp = 0, psp = 0, ssp = 0, lsp = 0;
+    const SdfInsn *code = S.sdf_insn;
+    const double *K = S.sdf_const;
+    while (pc < end) {
+        const SdfInsn I = code[pc];
+        switch (I.op) {
+        case SOP_END: pc = end; continue;
+        case SOP_BOX: {  // BoxSDF.distanceComp (sdf.js:276-279)
+            // q = p.abs().minus(size).to4(0); Vec.max(q, 0).norm() + min(max(q0,q1,q2), 0)
+            const float qx = fabsf(P.x) - (float)K[I.a];
+            const float qy = or0(fabsf(P.y) - (float)K[I.a + 1]);
+            const float qz = or0(fabsf(P.z) - (float)K[I.a + 2]);
+            const F3 m = f3((float)js_max(qx, 0), (float)js_max(qy, 0), (float)js_max(qz, 0));
+            dst[dsp++] = sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0);
+            break;
+        }
+        case SOP_SPHERE: {  // p.to4(0).norm() - radius (sdf.js:232-234)
+            const F3 q = f3(P.x, or0(P.y), or0(P.z));
+            dst[dsp++] = sqrt(dot3(q, q)) - K[I.a];
+            break;
+        }
+        case SOP_TETRA:  // sdf.js:305-308
+            dst[dsp++] = (js_max(fabs((double)P.x + (double)P.y) - (double)P.z,
+                                 fabs((double)P.x - (double)P.y) + (double)P.z) - 1) / sqrt(3.0);
+            break;
+        case SOP_MIN: {
+            double r = dst[dsp - I.a];
+            for (int i = 1; i < I.a; ++i) r = js_min(r, dst[dsp - I.a + i]);
+            dsp -= I.a;
+            dst[dsp++] = r;
+            break;
+        }
+        case SOP_MAX: {
+            double r = dst[dsp - I.a];
+            for (int i = 1; i < I.a; ++i) r = js_max(r, dst[dsp - I.a + i]);
+            dsp -= I.a;
+            dst[dsp++] = r;
+            break;
+        }
+        case SOP_NEG: dst[dsp - 1] = -dst[dsp - 1]; break;
+        case SOP_SUBK: dst[dsp - 1] = dst[dsp - 1] - K[I.a]; break;
+        case SOP_SMIN: {  // smoothMin (sdf.js:128-131)
+            const double b = dst[--dsp], a = dst[dsp - 1], k = K[I.a];
+            const double h = js_max(k - fabs(a - b), 0.0) / k;
+            dst[dsp - 1] = js_min(a, b) - h * h * h * k * (1.0 / 6.0);
+            break;
+        }
+        case SOP_PUSHP: pst[psp++] = P; break;
+        case SOP_POPP: P = pst[--psp]; break;
+        case SOP_TPUSH: sst[ssp++] = 1.0; break;
+        case SOP_TPOP: --ssp; break;
+        case SOP_TPOP_MUL: {
+            const double st = sst[--ssp];
+            sst[ssp - 1] = sst[ssp - 1] * st;
+            break;
+        }
+        case SOP_MULS: dst[dsp - 1] = dst[dsp - 1] * sst[ssp - 1]; break;
+        case SOP_XMAT:  // SDFMatrixTransformer.transform (sdf.js:433-435)
+            P = xf_point(K + I.a, P);
+            sst[ssp - 1] = sst[ssp - 1] * K[I.b];
+            break;
+        case SOP_XREF: {  // SDFReflectionTransformer.transformComp (sdf.js:450-455)
+            const F3 n = f3((float)K[I.a], (float)K[I.a + 1], (float)K[I.a + 2]);
+            const double dt = dot3(n, P) - K[I.a + 3];
+            if (dt < 0) P = sub(P, scale(n, 2 * dt));
+            break;
+        }
+        case SOP_XREP: {  // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473)
+            const double sx = K[I.a], sy = K[I.a + 1], sz = K[I.a + 2];
+            const float x = (float)(js_fmod((double)P.x + sx / 2, sx) - sx / 2);
+            const float y = (float)(js_fmod((double)P.y + sy / 2, sy) - sy / 2);
+            const float z = (float)(js_fmod((double)P.z + sz / 2, sz) - sz / 2);
+            P = f3(x, or0(y), or0(z));
+            break;
+        }
+        case SOP_LOOP:
+            if (I.a <= 0) { pc = I.b + 1; continue; }
+            lc[lsp++] = I.a;
+            break;
+        case SOP_ENDLOOP:
+            if (--lc[lsp - 1] > 0) { pc = I.a + 1; continue; }
+            --lsp;
+            break;
+        default: break;
+        }
+        ++pc;
+    }
+    return dst[0];
+}
+
+__device__ __forceinline__ double sdf_node_dist(const DScene &S, int n, F3 p) {
+    return sdf_run(S, S.sdf_range[2 * n], S.sdf_range[2 * n + 1], p);
+}
+
+__device__ double sdf_intersect(const DScene &S, int g, F3 o, F3 d, double minD, double maxD) {  // sdf.js:12-40
+    const jsrt_rec_sdfgeom &G = S.sdfg[g];
+    double bmin, bmax;
+    if (!aabb_slab(G.center[0], G.center[1], G.center[2], G.half[0], G.half[1], G.half[2], o, d, minD, maxD, bmin,
+                   bmax))
+        return -DINF;
+    minD = js_max(minD, bmin);
+    maxD = js_min(maxD, bmax);
+    double t = minD;
+    const double rd_norm = sqrt(dot3(d, d));
+    for (int i = 0; i < G.max_samples; ++i) {
+        const F3 p = ray_point(o, d, t);
+        const double distance = sdf_node_dist(S, G.root, p);
+        if (!__builtin_isfinite(distance)) break;
+        if (distance <= G.eps) return t;
+        t += distance / rd_norm;
+        if (t < minD || t > maxD || (t - minD) * rd_norm > G.max_trace) break;
+    }
+    return -DINF;
+}
+
+// SDF getMaterialData (sdf.js:87-360).  Smooth combinators blend both subtrees' data, so the walk
+// keeps a small explicit stack of pending blends.
+struct SdfMD {
+    F3 bc;
+    float u, v;
+    int has_bc, has_uv;
+};
+
+__device__ SdfMD sdf_leaf_md(const DScene &S, const jsrt_rec_sdfnode &N, F3 p) {
+    SdfMD r;
+    r.bc = f3(N.basecolor[0], N.basecolor[1], N.basecolor[2]);
+    r.has_bc = 1;
+    r.has_uv = 0;
+    r.u = r.v = 0;
+    if (N.kind == JSRT_SDF_SPHERE) {  // UV: cartesianToSpherical(p.to4(0).normalized())
+        r.has_uv = 1;
+        cart_to_sph(normalized(f3(p.x, or0(p.y), or0(p.z))), r.u, r.v);
+    }
+    return r;
+}
+
+__device__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
+    // Iterative post-order over the (binary) blend nodes; simple selector nodes are followed in place.
+    struct Pending {
+        int node;      // smooth node waiting for its children
+        double mixf;
+        int stage;     // 0: evaluating child a, 1: evaluating child b
+        SdfMD a;
+    };
+    Pending stk[8];
+    int sp = 0;
+    int n = root;
+    SdfMD res;
+    for (int guard = 0; guard < 256; ++guard) {
+        const jsrt_rec_sdfnode &N = S.sdf_nodes[n];
+        bool leaf = false;
+        switch (N.kind) {
+        case JSRT_SDF_UNION:
+        case JSRT_SDF_INTERSECTION: {  // Math.indexOfMin / indexOfMax (math.js:53-70)
+            int best = 0;
+            double bv = N.kind == JSRT_SDF_UNION ? DINF : -DINF;
+            for (int i = 0; i < N.count; ++i) {
+                const double d = sdf_node_dist(S, S.sdf_child[N.first + i], p);
+                if (N.kind == JSRT_SDF_UNION ? (d < bv) : (d > bv)) { bv = d; best = i; }
+            }
+            n = S.sdf_child[N.first + best];
+            continue;
+        }
+        case JSRT_SDF_DIFFERENCE:
+            n = (sdf_node_dist(S, N.a, p) > -sdf_node_dist(S, N.b, p)) ? N.a : N.b;
+            continue;
+        case JSRT_SDF_ROUND:
+        case JSRT_SDF_TRANSFORM:
+        case JSRT_SDF_RECURSIVE_UNION: n = N.a; continue;
+        case JSRT_SDF_SMOOTH_UNION:
+        case JSRT_SDF_SMOOTH_INTERSECTION:
+        case JSRT_SDF_SMOOTH_DIFFERENCE: {
+            const double da = sdf_node_dist(S, N.a, p), db = sdf_node_dist(S, N.b, p), k = N.k;
+            double x, y;  // smoothMinBlend arguments (sdf.js:133-137, 151, 172, 193)
+            if (N.kind == JSRT_SDF_SMOOTH_UNION) { x = da; y = db; }
+            else if (N.kind == JSRT_SDF_SMOOTH_INTERSECTION) { x = -da; y = -db; }
+            else { x = -da; y = db; }
+            const double h = js_max(k - fabs(x - y), 0.0) / k;
+            const double m = h * h * h * 0.5;
+            double mixf = (x < y) ? m : (1.0 - m);
+            if (N.kind == JSRT_SDF_SMOOTH_INTERSECTION) mixf = 1.0 - mixf;
+            if (sp >= 8) return res;
+            stk[sp].node = n;
+            stk[sp].mixf = mixf;
+            stk[sp].stage = 0;
+            ++sp;
+            n = N.a;
+            continue;
+        }
+        default: leaf = true; res = sdf_leaf_md(S, N, p); break;
+        }
+        if (!leaf) break;
+        // unwind finished subtrees into pending blends (SDF.blendMaterialData, sdf.js:66-73)
+        while (sp > 0) {
+            Pending &T = stk[sp - 1];
+            if (T.stage == 0) {
+                T.a = res;
+                T.stage = 1;
+                n = S.sdf_nodes[T.node].b;
+                break;
+            }
+            const SdfMD a = T.a, b = res;
+            const double mixf = T.mixf;
+            --sp;
+            if (mixf <= 0.0) res = a;
+            else if (mixf >= 1.0) res = b;
+            else {
+                const F3 ca = a.has_bc ? a.bc : f3(1, 1, 1), cb = b.has_bc ? b.bc : f3(1, 1, 1);
+                const float ua = a.has_uv ? a.u : 0.0f, va = a.has_uv ? a.v : 0.0f;
+                const float ub = b.has_uv ? b.u : 0.0f, vb = b.has_uv ? b.v : 0.0f;
+                res.bc = f3((float)((1 - mixf) * ca.x + mixf * cb.x), (float)((1 - mixf) * ca.y + mixf * cb.y),
+                            (float)((1 - mixf) * ca.z + mixf * cb.z));
+                res.u = (float)((1 - mixf) * ua + mixf * ub);
+                res.v = (float)((1 - mixf) * va + mixf * vb);
+                res.has_bc = res.has_uv = 1;
+            }
+        }
+        if (sp == 0) return res;
+    }
+    return res;
+}
+
+// --------------------------------------------------------------------------------------------
+// world intersection (world.js:7-15, 116-124; aggregates.js:14-18, 43-49, 207-225)
+struct Hit {
+    double t;
+    int prim;
+    int ctx;
+};
+
+template <int PF>
+__device__ __forceinline__ double prim_intersect_local(const DScene &S, const DPrim &P, F3 o, F3 d, double minD,
+                                                       double maxD) {
+    switch (P.gkind) {
+    case JSRT_GEOM_PLANE: return plane_t(o, d);
+    case JSRT_GEOM_SQUARE: {  // geometry.js:287-291
+        const double t = plane_t(o, d);
+        const F3 p = ray_point(o, d, t);
+        return (-0.5f <= p.x && p.x <= 0.5f && -0.5f <= p.y && p.y <= 0.5f) ? t : -DINF;
+    }
+    case JSRT_GEOM_CIRCLE: {  // geometry.js:310-314; the w term of p - (0,0,0,1) is 0 for finite t
+        const double t = plane_t(o, d);
+        const F3 p = ray_point(o, d, t);
+        return (dot3(p, p) <= 1) ? t : -DINF;
+    }
+    case JSRT_GEOM_SPHERE: return sphere_static(o, d, minD);
+    case JSRT_GEOM_CYLINDER: {  // geometry.js:473-478 (rays masked by Vec.of(1,1,0,1))
+        const double oz = o.z, dz = d.z;
+        if (fabs(oz) > 1 && dz != 0) minD = js_max(minD, -(oz - js_sign(oz)) / dz);
+        const double t = sphere_static(f3(o.x, o.y, o.z * 0.0f), f3(d.x, d.y, d.z * 0.0f), minD);
+        return (fabs(oz + t * dz) <= 1) ? t : -DINF;
+    }
+    case JSRT_GEOM_AABB: {  // geometry.js:173-179
+        double tmin, tmax;
+        if (aabb_slab(P.center[0], P.center[1], P.center[2], P.half[0], P.half[1], P.half[2], o, d, minD, maxD, tmin,
+                      tmax))
+            return (tmin >= minD) ? tmin : tmax;
+        return -DINF;
+    }
+    case JSRT_GEOM_TRIANGLE:
+        if (PF & PF_TRI) return tri_intersect(S.tris[P.gindex], o, d);
+        return -DINF;
+    case JSRT_GEOM_SDF:
+        if (PF & PF_SDF) return sdf_intersect(S, P.gindex, o, d, minD, maxD);
+        return -DINF;
+    default: return -DINF;
+    }
+}
+
+// Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
+template <int PF>
+__device__ __forceinline__ double prim_intersect(const DScene &S, int pi, F3 o, F3 d, double minD, double maxD,
+                                                 bool transp) {
+    const DPrim &P = S.prims[pi];
+    if (!transp && !P.casts_shadow) return DINF;
+    return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
+}
+
+// BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
+template <int PF, bool ANY>
+__device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
+    Hit best{DINF, -1, I.ctx};
+    const bool fast = I.count != 0;
+    int stack[64];
+    int sp = 0;
+    stack[sp++] = I.first;
+    while (sp > 0) {
+        const DBvhNode N = S.bvh[stack[--sp]];
+        double tmn, tmx;
+        if (aabb_slab(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, d, minD, maxD, tmn, tmx) && tmn <= maxD && tmx >= minD &&
+            tmn <= best.t) {
+            if (N.b < 0) {
+                const int cnt = ~N.b;
+                for (int k = 0; k < cnt; ++k) {
+                    double t;
+                    if (fast) t = tri_intersect(S.tris[S.leaf_tris[N.a + k]], o, d);
+                    else t = prim_intersect<PF>(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp);
+                    if (t > minD && t < maxD && t < best.t) {
+                        best.t = t;
+                        best.prim = S.leaf_prims[N.a + k];
+                        if (ANY) return best;
+                    }
+                }
+            } else {
+                stack[sp++] = N.a;  // lesser, visited after the greater subtree
+                stack[sp++] = N.b;
+            }
+        }
+    }
+    return best;
+}
+
+// Aggregate / BVH instance below the top level (aggregates.js:14-18): members flattened in DFS
+// order into the caller's running closest hit (equivalent to nested first-minimum selection).
+template <int PF, bool ANY>
+__device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, double maxD, bool transp, Hit &best) {
+    struct Fr {
+        int inst, next;
+        F3 o, d;
+    };
+    Fr st[8];
+    int sp = 0;
+    {
+        const DInst &I = S.insts[inst];
+        st[sp++] = Fr{inst, 0, xf_point(S.mats + 12 * I.matrix, o), xf_dir(S.mats + 12 * I.matrix, d)};
+    }
+    while (sp > 0) {
+        Fr &f = st[sp - 1];
+        const DInst &I = S.insts[f.inst];
+        if (I.kind == INST_BVH) {
+            const Hit h = bvh_cast<PF, ANY>(S, I, f.o, f.d, minD, maxD, transp);
+            --sp;
+            if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
+                best = h;
+                if (ANY) return;
+            }
+            continue;
+        }
+        if (f.next >= I.count) { --sp; continue; }
+        const int c = S.inst_child[I.first + f.next++];
+        const DInst &C = S.insts[c];
+        if (C.kind == INST_PRIM) {
+            const double t = prim_intersect<PF>(S, C.prim, f.o, f.d, minD, maxD, transp);
+            if (t > minD && t < best.t && t < maxD) {
+                best = Hit{t, C.prim, I.ctx};
+                if (ANY) return;
+            }
+        } else if (sp < 8) {
+            const double *m = S.mats + 12 * C.matrix;
+            const F3 no = xf_point(m, f.o), nd = xf_dir(m, f.d);
+            st[sp++] = Fr{c, 0, no, nd};
+        }
+    }
+}
+
+// World.cast (world.js:28-30); ANY = shadow query (only `0 < d < 1` of the closest is read,
+// materials.js:250-252, so the first accepted hit decides).
+//
+// Culling: every top-level object carries a world-space box inflated by a margin
+// >= 1e3 x the f32 rounding bound of any point the exact test can accept.  A lane skips an object
+// when its ray segment (minD, min(best, maxD)) provably misses that box, and the wave skips the
+// object when no lane needs it.  Skipped objects could not have produced an accepted hit, so the
+// closest hit (first minimum in World.objects order) is unchanged bit for bit.
+template <int PF, bool ANY>
+__device__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp) {
+    Hit best{DINF, -1, 0};
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
+    const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    const float fminD = (float)minD;
+    bool live = true;
+    for (int i = 0; i < S.n_roots; ++i) {
+        const RootBound &RB = S.rbounds[i];
+        bool need = live;
+        if (RB.bounded) {
+            const float e = RB.k * oabs + RB.e0;
+            float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
+            float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
+            a0 = (RB.lo[1] - e - o.y) * iy;
+            a1 = (RB.hi[1] + e - o.y) * iy;
+            tn = fmaxf(tn, fminf(a0, a1));
+            tf = fminf(tf, fmaxf(a0, a1));
+            a0 = (RB.lo[2] - e - o.z) * iz;
+            a1 = (RB.hi[2] + e - o.z) * iz;
+            tn = fmaxf(tn, fminf(a0, a1));
+            tf = fminf(tf, fmaxf(a0, a1));
+            const float lim = (float)(best.t < maxD ? best.t : maxD);
+            need = need && (tn <= tf) && (tf >= fminD) && (tn <= lim);
+        }
+        if (!__any(need)) continue;
+        if (!need) continue;
+        const int ri = S.roots[i];
+        const DInst &I = S.insts[ri];
+        if (I.kind == INST_PRIM) {
+            const double t = prim_intersect<PF>(S, I.prim, o, d, minD, maxD, transp);
+            if (t > minD && t < best.t && t < maxD) {
+                best = Hit{t, I.prim, 0};
+                if (ANY) live = false;
+            }
+        } else if (!(PF & (PF_BVH | PF_AGG))) {
+            continue;
+        } else if ((PF & PF_BVH) && I.kind == INST_BVH) {
+            const double *m = S.mats + 12 * I.matrix;
+            const Hit h = bvh_cast<PF, ANY>(S, I, xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
+            if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
+                best = h;
+                if (ANY) live = false;
+            }
+        } else if (PF & PF_AGG) {
+            nested_cast<PF, ANY>(S, ri, o, d, minD, maxD, transp, best);
+            if (ANY && best.prim >= 0) live = false;
+        }
+    }
+    return best;
+}
+
+// --------------------------------------------------------------------------------------------
+// materials (materials.js)
+__device__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
+    int chain[8];
+    int n = 0;
+    F3 c = f3(0, 0, 0);
+    for (int g = 0; g < 16; ++g) {
+        const jsrt_rec_mcolor &M = S.mc[m];
+        if (M.kind == JSRT_MC_SOLID) { c = f3(M.vec[0], M.vec[1], M.vec[2]); break; }
+        if (M.kind == JSRT_MC_CHECKER) {  // materials.js:72-75
+            const double r = js_fmod(floor((double)u) + floor((double)v), 2);
+            m = (fmod(r, 2.0) < 1) ? M.a : M.b;
+            continue;
+        }
+        if (n < 8) chain[n++] = m;
+        m = M.a;
+    }
+    for (int i = n - 1; i >= 0; --i) {  // ScaledMaterialColor: child.color(data).times(scale)
+        const jsrt_rec_mcolor &M = S.mc[chain[i]];
+        if (M.kind == JSRT_MC_SCALED_SCALAR) c = scale(c, M.scalar);
+        else c = mul(c, f3(M.vec[0], M.vec[1], M.vec[2]));
+    }
+    return c;
+}
+
+struct Child {
+    F3 dir, col, w;
+    double k;
+};
+
+struct ShadeData {    // material_data after getBaseFactors (materials.js:210-238, 302-308)
+    F3 pos, V, N, R, refr, ambient, diff, spec, refl, trans;
+    double vdotn, kr, smoothness;
+    bool backside, has_refr;
+};
+
+// PhongMaterial.colorFromLightSample / FresnelPhongMaterial.colorFromLightSample
+__device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, F3 dir, F3 lcol) {
+    const F3 L = normalized(dir);
+    double diffuse, specular;
+    if (mkind == JSRT_MAT_PHONG) {  // materials.js:261-269
+        diffuse = js_max(dot3(L, d.N), 0);
+        specular = js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
+    } else {  // materials.js:340-356
+        const double ldotn = dot3(L, d.N);
+        diffuse = 0;
+        specular = 0;
+        if (d.kr > 0 && ldotn >= 0) {
+            diffuse += d.kr * ldotn;
+            specular += d.kr * js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
+        }
+        if (d.kr < 1 && ldotn <= 0) {
+            diffuse += (1 - d.kr) * -ldotn;
+            specular += (1 - d.kr) * js_pow(js_max(dot3(L, d.refr), 0), d.smoothness);
+        }
+    }
+    return add(mul(lcol, scale(d.diff, diffuse)), mul(lcol, scale(d.spec, specular)));
+}
+
+// One sample of lights.js sampleIterator for `Lt` seen from world point P: the direction (delta, NOT
+// normalised: the shadow ray's t in (1e-4, 1) spans the segment) and the sample colour.
+__device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, F3 P, Rng &rng, F3 &delta, F3 &lcol) {
+    if (Lt.kind == JSRT_LIGHT_POINT) {  // SimplePointLight.sampleIterator (lights.js:45-53)
+        delta = sub(f3(Lt.pos[0], Lt.pos[1], Lt.pos[2]), P);
+        float u = 0, v = 0;
+        if (Lt.needs_uv) cart_to_sph(normalized(delta), u, v);
+        lcol = scale(mc_eval(S, Lt.color, u, v), 1 / (4 * JS_PI * dot3(delta, delta)));
+    } else {  // RandomSampleAreaLight.sampleIterator (lights.js:80-92)
+        F3 local;
+        if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Vec.spherePick().to4(1)
+            const double theta = 2.0 * JS_PI * rng.next();
+            const double phi = acos(2.0 * rng.next() - 1.0);
+            const double sin_phi = sin(phi);
+            local = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
+        } else {  // Square / Circle.sampleSurface (geometry.js:295-300, 326-331)
+            const double a = rng.next() - 0.5;
+            const double b = rng.next() - 0.5;
+            local = f3((float)a, (float)b, 0.0f);
+        }
+        const double *T = Lt.T;
+        const F3 wpos = f3((float)((((double)local.x * T[0] + (double)local.y * T[1]) + (double)local.z * T[2]) + T[3]),
+                           (float)((((double)local.x * T[4] + (double)local.y * T[5]) + (double)local.z * T[6]) + T[7]),
+                           (float)((((double)local.x * T[8] + (double)local.y * T[9]) + (double)local.z * T[10]) + T[11]));
+        delta = sub(wpos, P);
+        F3 wn;
+        float u, v;
+        if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Sphere.materialData: local.normalized() (w = 1 term included)
+            const double nn = sqrt(dot3(local, local) + 1.0);
+            F3 n = local;
+            float nw = 1.0f;
+            if (nn > 0.00001) { n = scale(local, 1 / nn); nw = (float)(1.0 * (1 / nn)); }
+            cart_to_sph(n, u, v);
+            const double *Ti = Lt.Ti;  // inv_transform.transposed().times(n).to4(0).normalized()
+            const float wx = (float)((((double)n.x * Ti[0] + (double)n.y * Ti[4]) + (double)n.z * Ti[8]) + (double)nw * Ti[12]);
+            const float wy = (float)((((double)n.x * Ti[1] + (double)n.y * Ti[5]) + (double)n.z * Ti[9]) + (double)nw * Ti[13]);
+            const float wz = (float)((((double)n.x * Ti[2] + (double)n.y * Ti[6]) + (double)n.z * Ti[10]) + (double)nw * Ti[14]);
+            wn = normalized(f3(wx, or0(wy), or0(wz)));
+        } else {
+            wn = f3(Lt.wn[0], Lt.wn[1], Lt.wn[2]);
+            u = local.x;
+            v = local.y;
+        }
+        const double sc = (1 / (4 * JS_PI * dot3(delta, delta))) * fabs(dot3(normalized(delta), wn));
+        lcol = scale(mc_eval(S, Lt.color, u, v), sc);
+    }
+}
+
+// PhongPathTracingMaterial.scatter (materials.js:398-412)
+__device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 R, F3 N, const ShadeData &d, Rng &rng,
+                                             F3 &dir, F3 &col) {
+    if (rng.next() < mirror_prob) {
+        dir = R;
+        col = f3(1, 1, 1);
+        return has_r;
+    }
+    const double dp = average3(d.diff), sp = average3(d.spec);
+    const double probSum = dp + sp;
+    if (probSum == 0) return false;
+    if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
+        const double theta = 2.0 * JS_PI * rng.next();
+        const double phi = acos(2.0 * rng.next() - 1.0);
+        const double sin_phi = sin(phi);
+        const F3 sp3 = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
+        dir = normalized(add(N, sp3));
+        col = scale(d.diff, 1 / JS_PI);
+        return true;
+    }
+    dir = R;  // scatterSpecular: finite smoothness returns R (materials.js:444-445)
+    col = d.spec;
+    return has_r;
+}
+
+
+// --------------------------------------------------------------------------------------------
+// Camera.getRayForPixel (cameras.js:29-34, 46-52)
+__device__ __forceinline__ void camera_ray(const DCamera &C, double x, double y, Rng &rng, F3 &o, F3 &d) {
+    const double *T = C.T;
+    const F3 dir = f3((float)(x * C.tan_fov * C.aspect), (float)(y * C.tan_fov), -1.0f);
+    o = f3((float)T[3], (float)T[7], (float)T[11]);
+    d = f3((float)((((double)dir.x * T[0] + (double)dir.y * T[1]) + (double)dir.z * T[2]) + 0.0 * T[3]),
+           (float)((((double)dir.x * T[4] + (double)dir.y * T[5]) + (double)dir.z * T[6]) + 0.0 * T[7]),
+           (float)((((double)dir.x * T[8] + (double)dir.y * T[9]) + (double)dir.z * T[10]) + 0.0 * T[11]));
+    if (C.kind == JSRT_CAMERA_DOF) {
+        const double a = rng.next() * 2 * JS_PI, rr = sqrt(rng.next());  // Vec.circlePick (math.js:175-179)
+        const float cx = (float)(rr * cos(a)), cy = (float)(rr * sin(a));
+        const float sx = (float)((double)cx * C.sensor), sy = or0((float)((double)cy * C.sensor));
+        const F3 off = f3((float)((((double)sx * T[0] + (double)sy * T[1]) + 0.0 * T[2]) + 0.0 * T[3]),
+                          (float)((((double)sx * T[4] + (double)sy * T[5]) + 0.0 * T[6]) + 0.0 * T[7]),
+                          (float)((((double)sx * T[8] + (double)sy * T[9]) + 0.0 * T[10]) + 0.0 * T[11]));
+        o = add(o, off);
+        d = normalized(sub(scale(d, C.focus), off));
+    }
+}
+
+__device__ __forceinline__ uint32_t set_color_rgba(F3 c) {  // PixelBuffer.setColor (pixelbuffer.js:39-49)
+    const float v[3] = {c.x, c.y, c.z};
+    uint32_t out = 0xFF000000u;  // alpha: colour length 3 -> comp 1 -> 255
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double comp = js_min(js_max((double)v[k], 0), 1);
+        const double r = js_round(255 * comp);
+        const uint32_t b = (r != r) ? 0u : (uint32_t)r;
+        out |= b << (8 * k);
+    }
+    return out;
+}
+
+
+}  // namespace jsrt

@@ -65,16 +65,16 @@ class Scene:
 
     @staticmethod
     def params(width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, device=0,
-               samples_per_launch=0, timelimit_ms=0.0):
+               samples_per_launch=0, timelimit_ms=0.0, max_paths=0):
         return Params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, device, samples_per_launch,
-                      timelimit_ms)
+                      timelimit_ms, max_paths)
 
     def render(self, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1,
-               samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0):
+               samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0, max_paths=0):
         """Render into host arrays.  Returns (rgba u8[H,W,4], colors f32[H,W,4] or None, stats)."""
         L = _native.lib()
         p = self.params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, self.device,
-                        samples_per_launch, timelimit_ms)
+                        samples_per_launch, timelimit_ms, max_paths)
         W = width if width > 0 else self.header()["width"]
         H = height if height > 0 else self.header()["height"]
         if rgba is None:

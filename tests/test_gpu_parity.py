@@ -78,13 +78,26 @@ def test_gpu_matches_oracle_larger(jr, case):
     assert st["samples"] == W * H * (spp if kind else 1)
 
 
-def test_gpu_progressive_chunks_equal_single_launch(jr):
-    """Splitting spp over launches (accumulator in HBM) must not change a bit."""
+def test_gpu_batching_is_invisible(jr):
+    """The wavefront schedule's batch size (paths per batch, incl. forced splitting of levels that
+    outgrow the pool) must not change a bit."""
     sc = _scene(jr, "cornell_box_path")
     a, ca, s1 = sc.render(40, 40, 6, 8, 1, 11)
-    b, cb, s2 = sc.render(40, 40, 6, 8, 1, 11, samples_per_launch=2)
-    assert s2["launches"] == 3 and s1["launches"] == 1
+    b, cb, s2 = sc.render(40, 40, 6, 8, 1, 11, max_paths=640)
+    assert s2["batches"] > s1["batches"] >= 1
     assert np.array_equal(a, b) and np.array_equal(ca.view(np.uint32), cb.view(np.uint32))
+    c, cc, _ = _scene(jr, "bunny").render(48, 40, 2, 4, 1, 3, max_paths=64)  # Fresnel: 2 children per hit
+    d, cd, _ = _scene(jr, "bunny").render(48, 40, 2, 4, 1, 3)
+    assert np.array_equal(c, d) and np.array_equal(cc.view(np.uint32), cd.view(np.uint32))
+
+
+def test_gpu_progress_callback(jr):
+    """renderers.js:103-112: callback({pass, completion}) while rendering, completion increasing."""
+    sc = _scene(jr, "cornell_box_path")
+    seen = []
+    sc.render(64, 64, 8, 8, 1, 1, max_paths=4096, progress=lambda p, c: seen.append((p, c)), timelimit_ms=1e-6)
+    assert seen and all(0 < c < 1 for _, c in seen)
+    assert [c for _, c in seen] == sorted(c for _, c in seen)
 
 
 def test_gpu_partition_invariance(jr):
