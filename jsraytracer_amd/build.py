@@ -27,18 +27,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, variant=None, defines=()):
+    """variant: build _build/libjsrt_<variant>.so with extra -D defines (A/B experiments)."""
     os.makedirs(OUT, exist_ok=True)
-    if not force and not _stale():
+    lib = LIB if variant is None else os.path.join(OUT, f"libjsrt_{variant}.so")
+    if variant is None and not force and not _stale():
         return LIB
-    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
+    cmd = [HIPCC] + FLAGS + list(defines) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    print(LIB)
+    args = sys.argv[1:]
+    var = args[args.index("--variant") + 1] if "--variant" in args else None
+    print(build(force="--force" in args, verbose=True, variant=var, defines=[a for a in args if a.startswith("-D")]))

@@ -98,7 +98,8 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     const size_t o_prims = A.add(H.prims), o_insts = A.add(H.insts), o_ichild = A.add(H.inst_child),
                  o_roots = A.add(H.roots), o_rb = A.add(H.rbounds), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
                  o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
-                 o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
+                 o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_matf = A.add(H.mat_flags), o_ps = A.add(H.prim_shade),
+                 o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
                  o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg);
     const size_t total = A.host.size() + 256;
@@ -120,6 +121,10 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.tris = (const DTri *)(b + o_tris);
     D.trish = (const DTriShade *)(b + o_trish);
     D.mat = (const jsrt_rec_material *)(b + o_mat);
+    D.mat_flags = (const int32_t *)(b + o_matf);
+    D.prim_shade = (const int32_t *)(b + o_ps);
+    D.shade0 = (const double *)(b + o_sh0);
+    D.shadeI = (const double *)(b + o_shI);
     D.mc = (const jsrt_rec_mcolor *)(b + o_mc);
     D.lights = (const DLight *)(b + o_lights);
     D.sdf_insn = (const SdfInsn *)(b + o_insn);

@@ -53,7 +53,7 @@ __device__ __forceinline__ float or0(float x) { return (x != x || x == 0.0f) ? 0
 // Number(v.toPrecision(8)) — ECMA-262 toPrecision (ties -> larger n) then correctly rounded parse.
 // Exact for 1e-12 <= |v| < 2^64 (128-bit products, no 128-bit division); outside that window the
 // 8-digit rounding is applied in float64 (documented in DESIGN.md; no reference scene reaches it).
-__device__ double to_precision8(double v) {
+__device__ __forceinline__ double to_precision8(double v) {
     if (!__builtin_isfinite(v)) return v;
     if (v == 0.0) return 0.0;
     const bool neg = v < 0;
@@ -244,7 +244,7 @@ __device__ __forceinline__ double tri_intersect(const DTri &T, F3 o, F3 d) {  //
 
 // --------------------------------------------------------------------------------------------
 // SDF program VM (sdf_program.h).  P is the 4-vector point with w == 1.
-__device__ double sdf_run(const DScene &S, int pc, int end, F3 P) {
+__device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P) {
     double dst[SDF_MAX_D];
     F3 pst[SDF_MAX_P];
     double sst[SDF_MAX_S];
@@ -343,7 +343,7 @@ __device__ __forceinline__ double sdf_node_dist(const DScene &S, int n, F3 p) {
     return sdf_run(S, S.sdf_range[2 * n], S.sdf_range[2 * n + 1], p);
 }
 
-__device__ double sdf_intersect(const DScene &S, int g, F3 o, F3 d, double minD, double maxD) {  // sdf.js:12-40
+__device__ __forceinline__ double sdf_intersect(const DScene &S, int g, F3 o, F3 d, double minD, double maxD) {  // sdf.js:12-40
     const jsrt_rec_sdfgeom &G = S.sdfg[g];
     double bmin, bmax;
     if (!aabb_slab(G.center[0], G.center[1], G.center[2], G.half[0], G.half[1], G.half[2], o, d, minD, maxD, bmin,
@@ -372,7 +372,7 @@ struct SdfMD {
     int has_bc, has_uv;
 };
 
-__device__ SdfMD sdf_leaf_md(const DScene &S, const jsrt_rec_sdfnode &N, F3 p) {
+__device__ __forceinline__ SdfMD sdf_leaf_md(const DScene &S, const jsrt_rec_sdfnode &N, F3 p) {
     SdfMD r;
     r.bc = f3(N.basecolor[0], N.basecolor[1], N.basecolor[2]);
     r.has_bc = 1;
@@ -385,7 +385,7 @@ __device__ SdfMD sdf_leaf_md(const DScene &S, const jsrt_rec_sdfnode &N, F3 p) {
     return r;
 }
 
-__device__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
+__device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
     // Iterative post-order over the (binary) blend nodes; simple selector nodes are followed in place.
     struct Pending {
         int node;      // smooth node waiting for its children
@@ -529,7 +529,7 @@ __device__ __forceinline__ double prim_intersect(const DScene &S, int pi, F3 o, 
 
 // BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
 template <int PF, bool ANY>
-__device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
+__device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, I.ctx};
     const bool fast = I.count != 0;
     int stack[64];
@@ -564,7 +564,7 @@ __device__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD
 // Aggregate / BVH instance below the top level (aggregates.js:14-18): members flattened in DFS
 // order into the caller's running closest hit (equivalent to nested first-minimum selection).
 template <int PF, bool ANY>
-__device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, double maxD, bool transp, Hit &best) {
+__device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, double maxD, bool transp, Hit &best) {
     struct Fr {
         int inst, next;
         F3 o, d;
@@ -613,7 +613,7 @@ __device__ void nested_cast(const DScene &S, int inst, F3 o, F3 d, double minD, 
 // object when no lane needs it.  Skipped objects could not have produced an accepted hit, so the
 // closest hit (first minimum in World.objects order) is unchanged bit for bit.
 template <int PF, bool ANY>
-__device__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp) {
+__device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, 0};
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
@@ -666,7 +666,7 @@ __device__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD,
 
 // --------------------------------------------------------------------------------------------
 // materials (materials.js)
-__device__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
+__device__ __forceinline__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
     int chain[8];
     int n = 0;
     F3 c = f3(0, 0, 0);
@@ -701,8 +701,8 @@ struct ShadeData {    // material_data after getBaseFactors (materials.js:210-23
 };
 
 // PhongMaterial.colorFromLightSample / FresnelPhongMaterial.colorFromLightSample
-__device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, F3 dir, F3 lcol) {
-    const F3 L = normalized(dir);
+// L = the sample direction normalised (light_sample computes it once for both uses)
+__device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, F3 L, F3 lcol) {
     double diffuse, specular;
     if (mkind == JSRT_MAT_PHONG) {  // materials.js:261-269
         diffuse = js_max(dot3(L, d.N), 0);
@@ -725,11 +725,13 @@ __device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, 
 
 // One sample of lights.js sampleIterator for `Lt` seen from world point P: the direction (delta, NOT
 // normalised: the shadow ray's t in (1e-4, 1) spans the segment) and the sample colour.
-__device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, F3 P, Rng &rng, F3 &delta, F3 &lcol) {
+__device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, F3 P, Rng &rng, F3 &delta, F3 &L,
+                                             F3 &lcol) {
     if (Lt.kind == JSRT_LIGHT_POINT) {  // SimplePointLight.sampleIterator (lights.js:45-53)
         delta = sub(f3(Lt.pos[0], Lt.pos[1], Lt.pos[2]), P);
+        L = normalized(delta);
         float u = 0, v = 0;
-        if (Lt.needs_uv) cart_to_sph(normalized(delta), u, v);
+        if (Lt.needs_uv) cart_to_sph(L, u, v);
         lcol = scale(mc_eval(S, Lt.color, u, v), 1 / (4 * JS_PI * dot3(delta, delta)));
     } else {  // RandomSampleAreaLight.sampleIterator (lights.js:80-92)
         F3 local;
@@ -766,7 +768,8 @@ __device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, 
             u = local.x;
             v = local.y;
         }
-        const double sc = (1 / (4 * JS_PI * dot3(delta, delta))) * fabs(dot3(normalized(delta), wn));
+        L = normalized(delta);
+        const double sc = (1 / (4 * JS_PI * dot3(delta, delta))) * fabs(dot3(L, wn));
         lcol = scale(mc_eval(S, Lt.color, u, v), sc);
     }
 }

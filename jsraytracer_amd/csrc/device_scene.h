@@ -97,6 +97,8 @@ struct DCamera {         // cameras.js:18-53
     int32_t kind, pad[3];
 };
 
+enum { MATF_UV = 1 };  // material colours depend on (u, v): a checkerboard in some chain
+
 struct DScene {
     const DPrim *prims;
     const DInst *insts;
@@ -111,6 +113,10 @@ struct DScene {
     const DTri *tris;
     const DTriShade *trish;
     const jsrt_rec_material *mat;
+    const int32_t *mat_flags;    // MATF_* per material
+    const int32_t *prim_shade;   // per prim: -1 identity inv_transform, else its slot in shade0
+    const double *shade0;        // 16 per slot: prim.inv x identity (the ctx-0 shading matrix)
+    const double *shadeI;        // 16 per ctx: identity x ctx (shading matrix of identity prims)
     const jsrt_rec_mcolor *mc;
     const DLight *lights;
     const SdfInsn *sdf_insn;     // SDF programs (sdf_program.h)

@@ -27,28 +27,50 @@
 #include "device_common.h"
 #include "render_kernel.h"
 
+#ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade (register budget)
+#define JSRT_SHADE_OCC 2
+#endif
+#ifndef JSRT_SHADOW_OCC
+#define JSRT_SHADOW_OCC 1
+#endif
+#ifndef JSRT_EXTEND_OCC
+#define JSRT_EXTEND_OCC 1
+#endif
+
 namespace jsrt {
 
 const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final"};
-constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;
+constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;  // camera ray: its result is the path's root colour
+constexpr uint32_t DEAD_RAY = 0xFFFFFFFEu;   // level-0 slot of a path outside the image (no result)
 
-// wave-aggregated append: each lane appends n (0..2) entries; returns the lane's first index.
-__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, int n) {
+// block-aggregated append (one atomic per block: same-address atomics serialise device-wide).
+// Every thread of the block must call it.
+template <int NT>
+__device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t s_off[NW + 1];
     const uint64_t b1 = __ballot(n >= 1), b2 = __ballot(n >= 2);
-    const int lane = (int)__lane_id();
+    const int lane = (int)__lane_id(), wid = (int)(threadIdx.x >> 6);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t pre = (uint32_t)(__popcll(b1 & lt) + __popcll(b2 & lt));
-    const uint32_t tot = (uint32_t)(__popcll(b1) + __popcll(b2));
-    const uint64_t active = __ballot(1);
-    const int leader = __ffsll((long long)active) - 1;
-    uint32_t base = 0;
-    if (lane == leader && tot) base = atomicAdd(counter, tot);
-    base = __shfl(base, leader);
-    return base + pre;
+    if (lane == 0) s_off[wid] = (uint32_t)(__popcll(b1) + __popcll(b2));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = s_off[w];
+            s_off[w] = acc;
+            acc += c;
+        }
+        s_off[NW] = acc ? atomicAdd(counter, acc) : 0u;
+    }
+    __syncthreads();
+    return s_off[NW] + s_off[wid] + pre;
 }
 
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {
     const uint32_t p = W.parent[i];
+    if (p == DEAD_RAY) return;
     float *dst = (p == NO_PARENT) ? W.root + 3 * (size_t)W.path[i] : W.slot + 3 * (size_t)p;
     dst[0] = c.x;
     dst[1] = c.y;
@@ -69,27 +91,36 @@ __device__ __forceinline__ bool pixel_of(const RenderArgs &A, uint32_t p, int &c
 // Geometry.materialData + Material.color (materials.js).  Writes the node (info, ambient / surface,
 // shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
 template <int PF>
-__device__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t tt, const Hit &h, F3 o, F3 d,
+__device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t tt, const Hit &h, F3 o, F3 d,
                           uint32_t addr, uint32_t key, Child ch[2], F3 &pos) {
     const DPrim &P = S.prims[h.prim];
-    // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409)
+    // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409); the host
+    // precomputed it (same operations) for identity prims and for the top-level context
     double inv[16];
     {
-        const double *C = S.ctx + 16 * h.ctx;
+        const int ps = S.prim_shade[h.prim];
+        if (ps < 0 || h.ctx == 0) {
+            const double *src = ps < 0 ? S.shadeI + 16 * h.ctx : S.shade0 + 16 * ps;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int k = 0; k < 16; ++k) inv[k] = src[k];
+        } else {
+            const double *C = S.ctx + 16 * h.ctx;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const double a0 = r < 3 ? P.inv[4 * r + 0] : 0.0, a1 = r < 3 ? P.inv[4 * r + 1] : 0.0,
-                             a2 = r < 3 ? P.inv[4 * r + 2] : 0.0, a3 = r < 3 ? P.inv[4 * r + 3] : 1.0;
-                double s = 0;
-                s += a0 * C[c];
-                s += a1 * C[4 + c];
-                s += a2 * C[8 + c];
-                s += a3 * C[12 + c];
-                inv[4 * r + c] = s;
-            }
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const double a0 = r < 3 ? P.inv[4 * r + 0] : 0.0, a1 = r < 3 ? P.inv[4 * r + 1] : 0.0,
+                                 a2 = r < 3 ? P.inv[4 * r + 2] : 0.0, a3 = r < 3 ? P.inv[4 * r + 3] : 1.0;
+                    double s = 0;
+                    s += a0 * C[c];
+                    s += a1 * C[4 + c];
+                    s += a2 * C[8 + c];
+                    s += a3 * C[12 + c];
+                    inv[4 * r + c] = s;
+                }
+        }
     }
+    const bool need_uv = (S.mat_flags[P.material] & MATF_UV) != 0;
     const F3 lo = xf_point(inv, o), ld = xf_dir(inv, d);
     const F3 pl = ray_point(lo, ld, h.t);  // base_data.position (local)
     F3 nrm = f3(0, 0, 0);
@@ -109,13 +140,15 @@ __device__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t 
         nrm = pl;
         nrm_w = 1.0f;
         if (nn > 0.00001) { nrm = scale(pl, 1 / nn); nrm_w = (float)(1.0 * (1 / nn)); }
-        cart_to_sph(nrm, u, v);
+        if (need_uv) cart_to_sph(nrm, u, v);
         break;
     }
     case JSRT_GEOM_CYLINDER:  // geometry.js:479-487
         nrm = normalized(f3(pl.x, pl.y, 0));
-        u = (float)(0.5 + atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
-        v = (float)(0.5 + (double)pl.z);
+        if (need_uv) {
+            u = (float)(0.5 + atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
+            v = (float)(0.5 + (double)pl.z);
+        }
         break;
     case JSRT_GEOM_AABB: {  // geometry.js:210-224
         double norm_dist = 0;
@@ -257,9 +290,9 @@ __device__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t 
             const DLight &Lt = S.lights[li];
             const int ns = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
             for (int k = 0; k < ns; ++k, ++s) {
-                F3 delta, lcol;
-                light_sample(S, Lt, sd.pos, rng, delta, lcol);
-                const F3 c = light_sample_color(mkind, sd, delta, lcol);
+                F3 delta, L, lcol;
+                light_sample(S, Lt, sd.pos, rng, delta, L, lcol);
+                const F3 c = light_sample_color(mkind, sd, L, lcol);
                 const size_t e = (size_t)tt * W.ns + s;
                 W.sdx[e] = delta.x; W.sdy[e] = delta.y; W.sdz[e] = delta.z;
                 W.scx[e] = c.x; W.scy[e] = c.y; W.scz[e] = c.z;
@@ -290,20 +323,21 @@ __device__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t 
 
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
+    // level 0 holds one camera ray per path of the batch at slot q (no append); paths whose pixel
+    // lies outside the image (edge patches) get a DEAD_RAY slot that misses and writes nothing
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;  // path index in the batch
-    bool valid = q < W.npaths;
+    if (q >= W.npaths) return;
     int c = 0, py = 0, px = 0;
-    uint32_t smp = 0;
-    if (valid) {
-        const uint32_t pl = q % W.npix, sl = q / W.npix;  // sample-major: neighbours are neighbour pixels
-        smp = W.s0 + sl;
-        valid = pixel_of(A, W.p0 + pl, c, py, px);
-    }
-    const bool emit = valid && A.max_depth > 0;
-    const uint32_t at = wave_append(W.counter, emit ? 1 : 0);
-    if (!valid) return;
-    if (!emit) {  // World.color(ray, 0) = black
+    const uint32_t pl = q % W.npix, sl = q / W.npix;  // sample-major: neighbours are neighbour pixels
+    const uint32_t smp = W.s0 + sl;
+    const bool valid = pixel_of(A, W.p0 + pl, c, py, px);
+    if (A.max_depth <= 0) {  // World.color(ray, 0) = black; no level is traced
         W.root[3 * q] = W.root[3 * q + 1] = W.root[3 * q + 2] = 0.0f;
+        return;
+    }
+    W.path[q] = q;
+    if (!valid) {
+        W.parent[q] = DEAD_RAY;
         return;
     }
     const uint32_t pixel = (uint32_t)(py * A.W + px);
@@ -318,19 +352,22 @@ __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     }
     F3 o, d;
     camera_ray(S.cam, x, y, pre, o, d);
-    W.ox[at] = o.x; W.oy[at] = o.y; W.oz[at] = o.z;
-    W.dx[at] = d.x; W.dy[at] = d.y; W.dz[at] = d.z;
-    W.addr[at] = mix32(0u, 1u);
-    W.key[at] = key;
-    W.path[at] = q;
-    W.parent[at] = NO_PARENT;
+    W.ox[q] = o.x; W.oy[q] = o.y; W.oz[q] = o.z;
+    W.dx[q] = d.x; W.dy[q] = d.y; W.dz[q] = d.z;
+    W.addr[q] = mix32(0u, 1u);
+    W.key[q] = key;
+    W.parent[q] = NO_PARENT;
 }
 
 template <int PF>
-__global__ __launch_bounds__(256) void k_extend(DScene S, WArgs W, uint32_t base, uint32_t count, double minD) {
+__global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, uint32_t base, uint32_t count, double minD) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     if (t >= count) return;
     const uint32_t i = base + t;
+    if (W.parent[i] == DEAD_RAY) {
+        W.prim[i] = -1;
+        return;
+    }
     const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
     const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
     W.t[i] = h.t;
@@ -339,7 +376,7 @@ __global__ __launch_bounds__(256) void k_extend(DScene S, WArgs W, uint32_t base
 }
 
 template <int PF>
-__global__ __launch_bounds__(256) void k_shade(DScene S, WArgs W, uint32_t base, uint32_t count, int child_depth) {
+__global__ __launch_bounds__(256, JSRT_SHADE_OCC) void k_shade(DScene S, WArgs W, uint32_t base, uint32_t count, int child_depth) {
     const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
     const bool in = tt < count;
     const uint32_t i = base + (in ? tt : 0u);
@@ -363,7 +400,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene S, WArgs W, uint32_t base,
         }
     }
     // children: World.color(child, depth - 1); at depth 0 they are black without a cast
-    const uint32_t at = wave_append(W.counter, child_depth > 0 ? nchild : 0);
+    const uint32_t at = block_append<256>(W.counter, child_depth > 0 ? nchild : 0);
     if (!hit) return;
     const uint32_t path = W.path[i];
     for (int j = 0; j < nchild; ++j) {
@@ -387,7 +424,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene S, WArgs W, uint32_t base,
 
 // The shadow casts of a node's light samples (materials.js:250-252) + colorFromLights' sums.
 template <int PF>
-__global__ __launch_bounds__(256) void k_shadow(DScene S, WArgs W, uint32_t base, uint32_t count) {
+__global__ __launch_bounds__(256, JSRT_SHADOW_OCC) void k_shadow(DScene S, WArgs W, uint32_t base, uint32_t count) {
     const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
     if (tt >= count) return;
     const uint32_t i = base + tt;
@@ -559,11 +596,8 @@ hipError_t run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipSt
     std::vector<uint32_t> lvl_base, lvl_count;
     overflow = false;
     hipError_t e;
-    if ((e = hipMemsetAsync(W.counter, 0, 4, st)) != hipSuccess) return e;
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
-    if ((e = hipMemcpyAsync(h_counter, W.counter, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    uint32_t base = 0, count = *h_counter;
+    uint32_t base = 0, count = A.max_depth > 0 ? W.npaths : 0;
     for (int L = 0; L < A.max_depth && count > 0; ++L) {
         const uint32_t next = base + count;
         const int child_depth = A.max_depth - L - 1;

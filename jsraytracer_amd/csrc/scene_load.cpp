@@ -93,6 +93,22 @@ bool is_identity(const double *m) {
     return true;
 }
 
+// The shading matrix prim.inv x ctx exactly as render.hip's shade_node computes it (prim row 3
+// taken as 0,0,0,1; sums from 0, left to right, float64) — precomputed for the common cases.
+void shade_matrix(const double *pinv12, const double *C, double *out) {
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            const double a0 = r < 3 ? pinv12[4 * r + 0] : 0.0, a1 = r < 3 ? pinv12[4 * r + 1] : 0.0,
+                         a2 = r < 3 ? pinv12[4 * r + 2] : 0.0, a3 = r < 3 ? pinv12[4 * r + 3] : 1.0;
+            double s = 0;
+            s += a0 * C[c];
+            s += a1 * C[4 + c];
+            s += a2 * C[8 + c];
+            s += a3 * C[12 + c];
+            out[4 * r + c] = s;
+        }
+}
+
 // Mat*Mat exactly as math.js:399-409 (sum from 0, left to right, float64)
 void mat_mul(const double *A, const double *B, double *R) {
     double t[16];
@@ -203,6 +219,31 @@ struct Loader {
             break;
         case JSRT_MC_CHECKER: check_mc(m.a, depth + 1); check_mc(m.b, depth + 1); break;
         default: fail("unsupported material colour kind");
+        }
+    }
+
+    bool mc_uses_uv(int32_t i, int depth = 0) {
+        if (i < 0 || (uint32_t)i >= B.n_mc || depth > 8) return false;
+        const jsrt_rec_mcolor &m = B.mc[i];
+        if (m.kind == JSRT_MC_CHECKER) return true;
+        if (m.kind == JSRT_MC_SCALED_SCALAR || m.kind == JSRT_MC_SCALED_VEC) return mc_uses_uv(m.a, depth + 1);
+        return false;
+    }
+
+    void shading_matrices() {
+        static const double I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        S.prim_shade.assign(S.prims.size(), -1);
+        for (size_t p = 0; p < S.prims.size(); ++p) {
+            if (memcmp(S.prims[p].inv, I, sizeof I) == 0) continue;  // bitwise identity (no -0)
+            double m[16];
+            shade_matrix(S.prims[p].inv, S.ctx.data(), m);
+            S.prim_shade[p] = (int32_t)(S.shade0.size() / 16);
+            S.shade0.insert(S.shade0.end(), m, m + 16);
+        }
+        for (size_t c = 0; c < S.ctx.size() / 16; ++c) {
+            double m[16];
+            shade_matrix(I, S.ctx.data() + 16 * c, m);
+            S.shadeI.insert(S.shadeI.end(), m, m + 16);
         }
     }
 
@@ -685,6 +726,10 @@ struct Loader {
                     fail("infinite-smoothness path-tracing scatter is broken in the reference (materials.js:430)");
             }
             S.mat.push_back(M);
+            int32_t fl = 0;
+            for (int32_t root : {M.color, M.ambient, M.diffuse, M.specular, M.reflect, M.transmit})
+                if (mc_uses_uv(root)) fl |= MATF_UV;
+            S.mat_flags.push_back(fl);
         }
         for (uint32_t i = 0; i < B.n_mc; ++i) S.mc.push_back(B.mc[i]);
 
@@ -737,6 +782,7 @@ struct Loader {
             if (pr.gkind == JSRT_GEOM_TRIANGLE) f |= PF_TRI;
         }
         S.features = f;
+        shading_matrices();
         S.profile = f == 0 ? PF_ANALYTIC : (f & ~PF_MESH) == 0 ? PF_MESH : (f & ~PF_SDF) == 0 ? PF_SDF : PF_ALL;
         for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);
         if (B.n_sdf) S.sdf_child.assign(B.chld, B.chld + B.n_chld);

@@ -20,6 +20,9 @@ struct HostScene {
     std::vector<DTri> tris;
     std::vector<DTriShade> trish;
     std::vector<jsrt_rec_material> mat;
+    std::vector<int32_t> mat_flags;    // MATF_* per material
+    std::vector<int32_t> prim_shade;   // -1: identity inv_transform; else slot in shade0
+    std::vector<double> shade0, shadeI;  // 16 per slot / per ctx: precomputed shading matrices
     std::vector<jsrt_rec_mcolor> mc;
     std::vector<DLight> lights;
     std::vector<SdfInsn> sdf_insn;

@@ -1,19 +1,40 @@
-"""Summarise rocprofv3 --pmc csv passes for the render kernel (sum over its dispatches)."""
-import csv, glob, os, sys
+"""Summarise rocprofv3 --pmc csv passes per render kernel (k_gen, k_extend<PF>, k_shade<PF>, ...):
+counter sums over all dispatches of that kernel, plus derived per-wave figures."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
 root = sys.argv[1]
-tot = {}
-disp = {}
+tot, disp = {}, {}
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "render_kernel" not in row.get("Kernel_Name", ""):
+        m = re.search(r"jsrt::(k_\w+)(<[^>]*>)?", row.get("Kernel_Name", ""))
+        if not m:
             continue
+        k = m.group(1) + (m.group(2) or "")
         name = row["Counter_Name"]
-        tot[name] = tot.get(name, 0.0) + float(row["Counter_Value"])
-        disp.setdefault(name, set()).add(row.get("Dispatch_Id"))
+        tot.setdefault(k, {})
+        tot[k][name] = tot[k].get(name, 0.0) + float(row["Counter_Value"])
+        disp.setdefault(k, {}).setdefault(name, set()).add(row.get("Dispatch_Id"))
+out = {}
 for k in sorted(tot):
-    print(f"{k:32s} {tot[k]:.6g}  (dispatches {len(disp[k])})")
-v = tot.get("SQ_INSTS_VALU"); w = tot.get("SQ_WAVES")
-if v and w:
-    print(f"VALU insts per wave: {v / w:.4g}")
-if tot.get("SQ_THREAD_CYCLES_VALU") and tot.get("SQ_ACTIVE_INST_VALU"):
-    print(f"VALU lane utilisation: {tot['SQ_THREAD_CYCLES_VALU'] / (64 * tot['SQ_ACTIVE_INST_VALU']):.3f}")
+    t = tot[k]
+    print(f"== {k}")
+    for c in sorted(t):
+        print(f"   {c:28s} {t[c]:.6g}  (dispatches {len(disp[k][c])})")
+    w = t.get("SQ_WAVES")
+    if w:
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"):
+            if c in t:
+                print(f"   {c + ' / wave':28s} {t[c] / w:.5g}")
+        for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if c in t:
+                print(f"   {c + ' / wave (x4 cyc)':28s} {4 * t[c] / w:.5g}")
+    if t.get("SQ_THREAD_CYCLES_VALU") and t.get("SQ_ACTIVE_INST_VALU"):
+        print(f"   VALU lane utilisation        {t['SQ_THREAD_CYCLES_VALU'] / (64 * t['SQ_ACTIVE_INST_VALU']):.3f}")
+    out[k] = t
+with open(os.path.join(root, "summary.json"), "w") as f:
+    json.dump(out, f, indent=1)
