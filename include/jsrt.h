@@ -53,7 +53,7 @@ typedef struct {
     uint64_t samples;        /* pixel-samples rendered */
     uint32_t launches;       /* render-kernel launches */
     uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
-    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final */
+    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, lightsum */
     uint32_t stage_launches[JSRT_STAGES];
 } jsrt_stats;
 

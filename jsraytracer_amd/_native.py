@@ -23,7 +23,7 @@ class Params(ctypes.Structure):
                 ("max_paths", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
 
 
-STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "unused"]
+STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_lightsum"]
 
 
 class Stats(ctypes.Structure):
@@ -34,8 +34,8 @@ class Stats(ctypes.Structure):
     def as_dict(self):
         return {"kernel_ms": self.kernel_ms, "total_ms": self.total_ms, "samples": int(self.samples),
                 "launches": int(self.launches), "batches": int(self.batches),
-                "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(7)},
-                "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(7)}}
+                "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(8)},
+                "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(8)}}
 
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)

@@ -100,6 +100,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
                  o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
                  o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_matf = A.add(H.mat_flags), o_ps = A.add(H.prim_shade),
                  o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
+                 o_sl = A.add(H.sample_light), o_sc = A.add(H.sample_call),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
                  o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg);
     const size_t total = A.host.size() + 256;
@@ -127,6 +128,9 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.shadeI = (const double *)(b + o_shI);
     D.mc = (const jsrt_rec_mcolor *)(b + o_mc);
     D.lights = (const DLight *)(b + o_lights);
+    D.sample_light = (const int32_t *)(b + o_sl);
+    D.sample_call = (const int32_t *)(b + o_sc);
+    D.light_draws = H.light_draws;
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);
@@ -141,7 +145,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     memcpy(D.bg, H.bg, sizeof D.bg);
     D.all_roots_prims = H.all_roots_prims;
     D.profile = H.profile;
-    for (const DLight &L : H.lights) sc->ns += L.kind == JSRT_LIGHT_POINT ? 1 : L.samples;
+    sc->ns = (int)H.sample_light.size();
     *out = sc.release();
     return 0;
 }

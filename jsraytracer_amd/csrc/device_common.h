@@ -667,22 +667,36 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
 // --------------------------------------------------------------------------------------------
 // materials (materials.js)
 __device__ __forceinline__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
-    int chain[8];
-    int n = 0;
-    F3 c = f3(0, 0, 0);
-    for (int g = 0; g < 16; ++g) {
-        const jsrt_rec_mcolor &M = S.mc[m];
-        if (M.kind == JSRT_MC_SOLID) { c = f3(M.vec[0], M.vec[1], M.vec[2]); break; }
+    // walk Scaled* wrappers (and checkerboard choices) down to the solid colour, then apply the
+    // scales innermost first: ScaledMaterialColor.color = child.color(data).times(scale)
+    auto step = [&](int x) {  // next record below x (checkerboards resolved by (u, v))
+        const jsrt_rec_mcolor &M = S.mc[x];
         if (M.kind == JSRT_MC_CHECKER) {  // materials.js:72-75
             const double r = js_fmod(floor((double)u) + floor((double)v), 2);
-            m = (fmod(r, 2.0) < 1) ? M.a : M.b;
-            continue;
+            return (fmod(r, 2.0) < 1) ? M.a : M.b;
         }
-        if (n < 8) chain[n++] = m;
-        m = M.a;
+        return M.a;
+    };
+    int n = 0, x = m;  // n = number of Scaled wrappers on the way down
+    for (int g = 0; g < 16; ++g) {
+        const int k = S.mc[x].kind;
+        if (k == JSRT_MC_SOLID) break;
+        if (k != JSRT_MC_CHECKER) ++n;
+        x = step(x);
     }
-    for (int i = n - 1; i >= 0; --i) {  // ScaledMaterialColor: child.color(data).times(scale)
-        const jsrt_rec_mcolor &M = S.mc[chain[i]];
+    const jsrt_rec_mcolor &B = S.mc[x];
+    F3 c = f3(B.vec[0], B.vec[1], B.vec[2]);
+    for (int i = n - 1; i >= 0; --i) {  // the i-th wrapper from the top (usually n <= 1)
+        int y = m, seen = 0;
+        for (int g = 0; g < 16; ++g) {
+            const int k = S.mc[y].kind;
+            if (k != JSRT_MC_CHECKER) {
+                if (seen == i) break;
+                ++seen;
+            }
+            y = step(y);
+        }
+        const jsrt_rec_mcolor &M = S.mc[y];
         if (M.kind == JSRT_MC_SCALED_SCALAR) c = scale(c, M.scalar);
         else c = mul(c, f3(M.vec[0], M.vec[1], M.vec[2]));
     }

@@ -130,7 +130,10 @@ struct DScene {
     float bg[4];
     int32_t all_roots_prims; // every root is an INST_PRIM (uniform fast path)
     int32_t profile;         // PF_* feature set the kernel is instantiated for
-    int32_t pad[2];
+    const int32_t *sample_light;  // per light sample s of a node (lights in order): its light
+    const int32_t *sample_call;   // ... and the RNG call index of its first draw
+    int32_t light_draws;     // RNG draws of all light samples of a node (scatter draws follow)
+    int32_t pad[3];
 };
 
 }  // namespace jsrt

@@ -39,7 +39,8 @@
 
 namespace jsrt {
 
-const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final"};
+const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final",
+                                    "k_lightsum"};
 constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;  // camera ray: its result is the path's root colour
 constexpr uint32_t DEAD_RAY = 0xFFFFFFFEu;   // level-0 slot of a path outside the image (no result)
 
@@ -87,12 +88,17 @@ __device__ __forceinline__ bool pixel_of(const RenderArgs &A, uint32_t p, int &c
     return px < A.W;
 }
 
+__device__ __forceinline__ F3 pick(bool f, F3 a, F3 b) { return f3(f ? a.x : b.x, f ? a.y : b.y, f ? a.z : b.z); }
+__device__ __forceinline__ Child pick(bool f, const Child &a, const Child &b) {
+    return Child{pick(f, a.dir, b.dir), pick(f, a.col, b.col), pick(f, a.w, b.w), f ? a.k : b.k};
+}
+
 // World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
 // Geometry.materialData + Material.color (materials.js).  Writes the node (info, ambient / surface,
 // shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
 template <int PF>
 __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t tt, const Hit &h, F3 o, F3 d,
-                          uint32_t addr, uint32_t key, Child ch[2], F3 &pos) {
+                          uint32_t addr, uint32_t key, Child &ch0, Child &ch1, F3 &pos) {
     const DPrim &P = S.prims[h.prim];
     // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409); the host
     // precomputed it (same operations) for identity prims and for the top-level context
@@ -154,6 +160,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
         double norm_dist = 0;
         const float pc[3] = {pl.x, pl.y, pl.z};
         float nn[3] = {0, 0, 0};
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double comp = ((double)pc[i] - (double)P.center[i]) / (double)P.half[i];
             const double ac = fabs(comp);
@@ -228,7 +235,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
     if (mkind == JSRT_MAT_TRANSPARENT) {  // materials.js:169-173
         const F3 a = scale(mc_eval(S, M.color, u, v), M.opacity);
         W.sx[i] = a.x; W.sy[i] = a.y; W.sz[i] = a.z;
-        ch[0] = Child{d, f3(1, 1, 1), f3(1, 1, 1), 1 - M.opacity};
+        ch0 = Child{d, f3(1, 1, 1), f3(1, 1, 1), 1 - M.opacity};
         W.info[i] = INFO_HIT | (1u << INFO_NCHILD_SHIFT);
         return 1;
     }
@@ -278,43 +285,45 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
             sd.refr = add(scale(neg(sd.V), r), scale(Nn, r * vdotn - sqrt(k)));
         }
     }
-    // colorFromLights (materials.js:240-259): draw every light sample now (the draws of a node
-    // come before its scatter draws), cast the shadows in k_shadow
+    // colorFromLights (materials.js:240-259): k_shadow evaluates the light samples (one lane each,
+    // RNG calls [0, light_draws) of this frame) from the material data handed off here; the
+    // scatter draws below follow them (calls light_draws, ...)
     W.sx[i] = sd.ambient.x; W.sy[i] = sd.ambient.y; W.sz[i] = sd.ambient.z;
     uint32_t info = INFO_HIT;
     if (W.ns > 0) {
         info |= INFO_LIT;
         W.sox[tt] = sd.pos.x; W.soy[tt] = sd.pos.y; W.soz[tt] = sd.pos.z;
-        int s = 0;
-        for (int li = 0; li < S.n_lights; ++li) {
-            const DLight &Lt = S.lights[li];
-            const int ns = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
-            for (int k = 0; k < ns; ++k, ++s) {
-                F3 delta, L, lcol;
-                light_sample(S, Lt, sd.pos, rng, delta, L, lcol);
-                const F3 c = light_sample_color(mkind, sd, L, lcol);
-                const size_t e = (size_t)tt * W.ns + s;
-                W.sdx[e] = delta.x; W.sdy[e] = delta.y; W.sdz[e] = delta.z;
-                W.scx[e] = c.x; W.scy[e] = c.y; W.scz[e] = c.z;
-            }
-        }
+        W.fnx[tt] = sd.N.x; W.fny[tt] = sd.N.y; W.fnz[tt] = sd.N.z;
+        W.frx[tt] = sd.R.x; W.fry[tt] = sd.R.y; W.frz[tt] = sd.R.z;
+        W.ftx[tt] = sd.refr.x; W.fty[tt] = sd.refr.y; W.ftz[tt] = sd.refr.z;
+        W.fdx[tt] = sd.diff.x; W.fdy[tt] = sd.diff.y; W.fdz[tt] = sd.diff.z;
+        W.fsx[tt] = sd.spec.x; W.fsy[tt] = sd.spec.y; W.fsz[tt] = sd.spec.z;
+        W.fkr[tt] = sd.kr;
+        W.fmat[tt] = P.material;
+        rng.calls = (uint32_t)S.light_draws;
     }
     int n = 0;
+    auto push = [&](const Child &c) {  // unconditional selects keep both slots in registers
+        const bool first = n == 0;
+        ch0 = pick(first, c, ch0);
+        ch1 = pick(first, ch1, c);
+        ++n;
+    };
     if (mkind == JSRT_MAT_PHONG) {  // materials.js:277-288
-        if (dot3(sd.refl, sd.refl) > 0) ch[n++] = Child{sd.R, f3(1, 1, 1), sd.refl, 1.0};
-        if (dot3(sd.trans, sd.trans) > 0) ch[n++] = Child{normalized(d), f3(1, 1, 1), sd.trans, 1.0};
+        if (dot3(sd.refl, sd.refl) > 0) push(Child{sd.R, f3(1, 1, 1), sd.refl, 1.0});
+        if (dot3(sd.trans, sd.trans) > 0) push(Child{normalized(d), f3(1, 1, 1), sd.trans, 1.0});
     } else {  // materials.js:315-330
         if (sd.kr > 0) {
             F3 dir = sd.R, col = f3(1, 1, 1);
             bool ok = true;
             if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col);
-            if (ok) ch[n++] = Child{dir, col, sd.refl, sd.kr};
+            if (ok) push(Child{dir, col, sd.refl, sd.kr});
         }
         if (sd.kr < 1) {
             F3 dir = sd.refr, col = f3(1, 1, 1);
             bool ok = sd.has_refr;
             if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col);
-            if (ok) ch[n++] = Child{dir, col, sd.trans, 1 - sd.kr};
+            if (ok) push(Child{dir, col, sd.trans, 1 - sd.kr});
         }
     }
     W.info[i] = info | ((uint32_t)n << INFO_NCHILD_SHIFT);
@@ -381,7 +390,7 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) void k_shade(DScene S, WArgs W
     const bool in = tt < count;
     const uint32_t i = base + (in ? tt : 0u);
     int nchild = 0;
-    Child ch[2];
+    Child ch0, ch1;
     F3 pos = f3(0, 0, 0);
     uint32_t addr = 0, key = 0;
     bool hit = false;
@@ -396,53 +405,82 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) void k_shade(DScene S, WArgs W
             addr = W.addr[i];
             key = W.key[i];
             const Hit h{W.t[i], prim, W.ctx[i]};
-            nchild = shade_node<PF>(S, W, i, tt, h, o, d, addr, key, ch, pos);
+            nchild = shade_node<PF>(S, W, i, tt, h, o, d, addr, key, ch0, ch1, pos);
         }
     }
     // children: World.color(child, depth - 1); at depth 0 they are black without a cast
     const uint32_t at = block_append<256>(W.counter, child_depth > 0 ? nchild : 0);
     if (!hit) return;
     const uint32_t path = W.path[i];
-    for (int j = 0; j < nchild; ++j) {
-        const uint32_t sl = 2 * i + (uint32_t)j;
-        W.ccol[3 * sl] = ch[j].col.x; W.ccol[3 * sl + 1] = ch[j].col.y; W.ccol[3 * sl + 2] = ch[j].col.z;
-        W.cw[3 * sl] = ch[j].w.x; W.cw[3 * sl + 1] = ch[j].w.y; W.cw[3 * sl + 2] = ch[j].w.z;
-        W.ck[sl] = ch[j].k;
+    auto emit = [&](const Child &c, uint32_t j) {
+        const uint32_t sl = 2 * i + j;
+        W.ccol[3 * sl] = c.col.x; W.ccol[3 * sl + 1] = c.col.y; W.ccol[3 * sl + 2] = c.col.z;
+        W.cw[3 * sl] = c.w.x; W.cw[3 * sl + 1] = c.w.y; W.cw[3 * sl + 2] = c.w.z;
+        W.ck[sl] = c.k;
         if (child_depth > 0) {
-            const uint32_t r = at + (uint32_t)j;
+            const uint32_t r = at + j;
             W.ox[r] = pos.x; W.oy[r] = pos.y; W.oz[r] = pos.z;
-            W.dx[r] = ch[j].dir.x; W.dy[r] = ch[j].dir.y; W.dz[r] = ch[j].dir.z;
-            W.addr[r] = mix32(addr, (uint32_t)(j + 1));
+            W.dx[r] = c.dir.x; W.dy[r] = c.dir.y; W.dz[r] = c.dir.z;
+            W.addr[r] = mix32(addr, j + 1);
             W.key[r] = key;
             W.path[r] = path;
             W.parent[r] = sl;
         } else {
             W.slot[3 * sl] = W.slot[3 * sl + 1] = W.slot[3 * sl + 2] = 0.0f;
         }
-    }
+    };
+    if (nchild > 0) emit(ch0, 0);
+    if (nchild > 1) emit(ch1, 1);
 }
 
-// The shadow casts of a node's light samples (materials.js:250-252) + colorFromLights' sums.
+// One light sample of a lit node per lane (lane e = level index * ns + sample): the sample
+// (lights.js sampleIterator), its shadow cast (materials.js:250-252) and, when unshadowed,
+// colorFromLightSample (materials.js:261-269, 340-356); shadowed samples contribute 0.
 template <int PF>
 __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) void k_shadow(DScene S, WArgs W, uint32_t base, uint32_t count) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ns = (uint32_t)W.ns;
+    if (e >= count * ns) return;
+    const uint32_t tt = e / ns, s = e - tt * ns, i = base + tt;
+    if (!(W.info[i] & INFO_LIT)) return;
+    const F3 P = f3(W.sox[tt], W.soy[tt], W.soz[tt]);
+    const DLight &Lt = S.lights[S.sample_light[s]];
+    Rng rng{W.key[i], W.addr[i], (uint32_t)S.sample_call[s]};
+    F3 delta, L, lcol;
+    light_sample(S, Lt, P, rng, delta, L, lcol);
+    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
+    F3 c = f3(0, 0, 0);
+    if (!(sh.prim >= 0 && sh.t > 0 && sh.t < 1)) {
+        ShadeData sd;
+        sd.N = f3(W.fnx[tt], W.fny[tt], W.fnz[tt]);
+        sd.R = f3(W.frx[tt], W.fry[tt], W.frz[tt]);
+        sd.refr = f3(W.ftx[tt], W.fty[tt], W.ftz[tt]);
+        sd.diff = f3(W.fdx[tt], W.fdy[tt], W.fdz[tt]);
+        sd.spec = f3(W.fsx[tt], W.fsy[tt], W.fsz[tt]);
+        sd.kr = W.fkr[tt];
+        const jsrt_rec_material &M = S.mat[W.fmat[tt]];
+        sd.smoothness = M.smoothness;
+        c = light_sample_color((int)M.kind, sd, L, lcol);
+    }
+    W.scx[e] = c.x;
+    W.scy[e] = c.y;
+    W.scz[e] = c.z;
+}
+
+// colorFromLights' sums (materials.js:244-257): per light, its samples in order (a shadowed
+// sample adds +0, which never changes an f32 running sum that starts at +0), times 1/samples.
+__global__ __launch_bounds__(256) void k_lightsum(DScene S, WArgs W, uint32_t base, uint32_t count) {
     const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
     if (tt >= count) return;
     const uint32_t i = base + tt;
     if (!(W.info[i] & INFO_LIT)) return;
-    const F3 P = f3(W.sox[tt], W.soy[tt], W.soz[tt]);
     F3 ret = f3(W.sx[i], W.sy[i], W.sz[i]);  // ambient
-    int s = 0;
+    size_t e = (size_t)tt * W.ns;
     for (int li = 0; li < S.n_lights; ++li) {
         const DLight &Lt = S.lights[li];
         const int ns = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
         F3 light_color = f3(0, 0, 0);
-        for (int k = 0; k < ns; ++k, ++s) {
-            const size_t e = (size_t)tt * W.ns + s;
-            const F3 dir = f3(W.sdx[e], W.sdy[e], W.sdz[e]);
-            const Hit sh = world_cast<PF, true>(S, P, dir, 0.0001, 1, false);
-            if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) continue;
-            light_color = add(light_color, f3(W.scx[e], W.scy[e], W.scz[e]));
-        }
+        for (int k = 0; k < ns; ++k, ++e) light_color = add(light_color, f3(W.scx[e], W.scy[e], W.scz[e]));
         if (ns > 0) ret = add(ret, scale(light_color, 1.0 / ns));
     }
     W.sx[i] = ret.x;
@@ -549,7 +587,7 @@ hipError_t Wavefront::reserve(size_t pool, size_t level_cap, int ns) {
     bytes += 10 * need(pool, 4) + need(pool, 8) + 2 * need(pool, 4);  // rays + hits
     bytes += 4 * need(pool, 4);                                      // info + surface
     bytes += 3 * need(6 * pool, 4) + need(2 * pool, 8);              // ccol cw slot + ck
-    bytes += 3 * need(level_cap, 4) + 6 * need(level_cap * (size_t)ns, 4);
+    bytes += 18 * need(level_cap, 4) + need(level_cap, 8) + need(level_cap, 4) + 3 * need(level_cap * (size_t)ns, 4);
     bytes += need(3 * level_cap, 4) + 256;
     if (mem) (void)hipFree(mem);
     mem = nullptr;
@@ -572,8 +610,14 @@ hipError_t Wavefront::reserve(size_t pool, size_t level_cap, int ns) {
     w.ccol = carve<float>(p, 6 * pool); w.cw = carve<float>(p, 6 * pool); w.slot = carve<float>(p, 6 * pool);
     w.ck = carve<double>(p, 2 * pool);
     w.sox = carve<float>(p, level_cap); w.soy = carve<float>(p, level_cap); w.soz = carve<float>(p, level_cap);
+    w.fnx = carve<float>(p, level_cap); w.fny = carve<float>(p, level_cap); w.fnz = carve<float>(p, level_cap);
+    w.frx = carve<float>(p, level_cap); w.fry = carve<float>(p, level_cap); w.frz = carve<float>(p, level_cap);
+    w.ftx = carve<float>(p, level_cap); w.fty = carve<float>(p, level_cap); w.ftz = carve<float>(p, level_cap);
+    w.fdx = carve<float>(p, level_cap); w.fdy = carve<float>(p, level_cap); w.fdz = carve<float>(p, level_cap);
+    w.fsx = carve<float>(p, level_cap); w.fsy = carve<float>(p, level_cap); w.fsz = carve<float>(p, level_cap);
+    w.fkr = carve<double>(p, level_cap);
+    w.fmat = carve<int32_t>(p, level_cap);
     const size_t se = level_cap * (size_t)ns;
-    w.sdx = carve<float>(p, se); w.sdy = carve<float>(p, se); w.sdz = carve<float>(p, se);
     w.scx = carve<float>(p, se); w.scy = carve<float>(p, se); w.scz = carve<float>(p, se);
     w.root = carve<float>(p, 3 * level_cap);
     w.counter = carve<uint32_t>(p, 64);
@@ -616,10 +660,14 @@ hipError_t run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipSt
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL(k_shade<PF>, dim3(grid(count)), dim3(256), 0, st, S, W, base, count, child_depth);
         });
-        if (W.ns > 0)
+        if (W.ns > 0) {
             timed(KT_SHADOW, [&] {
-                hipLaunchKernelGGL(k_shadow<PF>, dim3(grid(count)), dim3(256), 0, st, S, W, base, count);
+                hipLaunchKernelGGL(k_shadow<PF>, dim3(grid((size_t)count * W.ns)), dim3(256), 0, st, S, W, base, count);
             });
+            timed(KT_LIGHTSUM, [&] {
+                hipLaunchKernelGGL(k_lightsum, dim3(grid(count)), dim3(256), 0, st, S, W, base, count);
+            });
+        }
         if ((e = hipMemcpyAsync(h_counter, W.counter, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
         base = next;
@@ -638,6 +686,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                         size_t max_paths, const std::function<bool(int, double)> &progress) {
     if (!A.accum) return hipErrorInvalidValue;
     const uint32_t npix_total = (uint32_t)A.patches * 64u;
+    if (ns > 4) max_paths = max_paths * 4 / (size_t)ns;  // the per-sample hand-off scales with ns
     if (max_paths < 64) max_paths = 64;
     uint32_t npix = npix_total, nsb = 1;  // batch: [p0, p0 + npix) pixels x [s0, s0 + nsb) samples
     if ((size_t)npix > max_paths) npix = (uint32_t)(max_paths & ~(size_t)63);

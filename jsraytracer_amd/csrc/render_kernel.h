@@ -45,9 +45,17 @@ struct WArgs {
     float *sx, *sy, *sz;  // ambient, then resolved surface colour
     float *ccol, *cw, *slot;  // [3 * (2 * i + j)]: child weights and child results
     double *ck;               // [2 * i + j]
-    // shade -> shadow hand-off of one level (index = ray index within the level)
-    float *sox, *soy, *soz;
-    float *sdx, *sdy, *sdz, *scx, *scy, *scz;  // [level_idx * ns + sample]
+    // shade -> shadow hand-off of one level (index = ray index within the level): the node's
+    // material_data after getBaseFactors, as colorFromLightSample reads it
+    float *sox, *soy, *soz;          // position (shadow-ray origin)
+    float *fnx, *fny, *fnz;          // N (flipped to the viewer's side)
+    float *frx, *fry, *frz;          // R
+    float *ftx, *fty, *ftz;          // refraction direction (0 when none)
+    float *fdx, *fdy, *fdz;          // diffuse colour (basecolor applied)
+    float *fsx, *fsy, *fsz;          // specular colour
+    double *fkr;                     // Fresnel reflection factor (1 for Phong)
+    int32_t *fmat;                   // material index
+    float *scx, *scy, *scz;          // [level_idx * ns + sample]: unshadowed sample colour or 0
     float *root;       // [3 * path]
     uint32_t *counter; // append counter of the next level
     // batch
@@ -66,7 +74,7 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     ~Wavefront();
 };
 
-enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_N };
+enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_LIGHTSUM, KT_N };
 extern const char *const KT_NAMES[KT_N];
 
 struct EventPairs {  // reusable HIP events bracketing every launch of one kernel kind

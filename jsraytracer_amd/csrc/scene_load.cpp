@@ -770,6 +770,14 @@ struct Loader {
                     fail("unsupported area light surface");
                 area_normal(L.inv, d.wn);
             } else fail("unsupported light kind");
+            // colorFromLights order: the light's samples in turn; each area sample draws twice
+            const int32_t ns = L.kind == JSRT_LIGHT_POINT ? 1 : (int32_t)L.samples;
+            if (ns < 0 || S.sample_light.size() + (size_t)ns > 4096) fail("too many light samples per shading point");
+            for (int32_t k = 0; k < ns; ++k) {
+                S.sample_light.push_back((int32_t)S.lights.size());
+                S.sample_call.push_back(S.light_draws);
+                if (L.kind == JSRT_LIGHT_AREA) S.light_draws += 2;
+            }
             S.lights.push_back(d);
         }
         int32_t f = 0;

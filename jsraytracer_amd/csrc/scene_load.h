@@ -25,6 +25,8 @@ struct HostScene {
     std::vector<double> shade0, shadeI;  // 16 per slot / per ctx: precomputed shading matrices
     std::vector<jsrt_rec_mcolor> mc;
     std::vector<DLight> lights;
+    std::vector<int32_t> sample_light, sample_call;  // per light sample of a node
+    int32_t light_draws = 0;
     std::vector<SdfInsn> sdf_insn;
     std::vector<double> sdf_const;
     std::vector<int32_t> sdf_range;
