@@ -3,16 +3,20 @@
 Workload (BASELINE.json configs[1]): tests/cornell_box_path, 1024x1024, 64 spp, maxRecursionDepth 8,
 IncrementalMultisamplingRenderer semantics, keyed RNG seed 1 — the reference's own scene graph
 (committed as tests/golden/scenes/cornell_box_path.jsrt.gz, exported from the live reference).
-A "step" renders one full frame (all 64 spp of every pixel) into HBM; with N GPUs the frame's columns
-are dealt to ranks in 16-column blocks (rank r owns blocks b with b % N == r) and gathered to rank 0
-over RCCL (torch.distributed nccl backend) — strong scaling of one fixed frame.
+A "step" renders one full frame (all 64 spp of every pixel) into HBM.  With N GPUs the frame's
+columns are dealt to ranks in 16-column blocks (jsraytracer_amd/tiles.py), each rank renders its
+tile, and the step ends with one gather of the tiles to rank 0 (RCCL over xGMI, nccl backend) plus the
+permute into image order — strong scaling of one fixed frame.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config cornell_box_path|dragon|bunny|SDF_Menger]
+    python bench.py [--gpus N --steps K --warmup W] [--config cornell_box_path|bunny|SDF_Menger|ASimpleScene]
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
-  roofline      — algorithmic bytes per launch (SURVEY.md §8(d) formula with counts measured by the
-                  oracle on the CPU-baseline sample) / measured launch time (HIP events on the render
-                  stream) vs 8 TB/s; traffic from committed rocprofv3 PMC passes when present.
+  roofline      — for the DOMINANT kernel (largest share of render-kernel time): SURVEY.md §8(d)
+                  algorithmic bytes per unit x units per launch / its average launch duration (HIP
+                  events on the render stream, measured live) vs 8 TB/s.  traffic = HBM bytes per launch
+                  from the committed rocprofv3 PMC passes (profiles/pmc_summary.json; FETCH_SIZE
+                  doubled per the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE).  The "valu"
+                  member carries the compute side, which binds for the analytic/SDF scenes.
   cpu_baseline  — the C oracle (port of the reference path) on a bounded column subsample, host cores.
 """
 import argparse
@@ -25,13 +29,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (scene, W, H, spp, kind, max_depth or None = scene's)
+    # name: (scene, W, H, spp, kind, max_depth)
     "cornell_box_path": ("cornell_box_path", 1024, 1024, 64, 1, 8),
     "bunny": ("bunny", 1920, 1080, 16, 1, 4),
     "SDF_Menger": ("SDF_Menger", 1024, 1024, 32, 1, 4),
     "ASimpleScene": ("ASimpleScene", 256, 256, 1, 1, 4),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (HBM3E 8 TB/s spec)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (HBM3E 8 TB/s spec)
+F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
+CLOCK_HZ = 2.4e9            # max clock, MI355X_MICROARCH.md chip table
+SIMDS = 256 * 4
+# issue cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md: f32 2 cyc; f64 at half
+# the f32 rate; transcendentals 4x)
+ISSUE_CYC = {"f64": 4.0, "trans_f64": 16.0, "trans_f32": 8.0, "other": 2.0}
 
 
 def env_int(name, default):
@@ -41,25 +51,32 @@ def env_int(name, default):
         return default
 
 
-def algorithmic_bytes_per_sample(counts, spp):
-    """node visits x 32 B + triangle tests x 64 B + top-level object tests x 128 B,
-    plus the per-pixel RGBA8 output (4 B) amortised over spp."""
-    return counts["node_visits"] * 32 + counts["tri_tests"] * 64 + counts["object_tests"] * 128 + 4.0 / spp
+def kernel_units(counts, kname):
+    """(units per pixel-sample, algorithmic bytes per unit, unit name) of one kernel, SURVEY.md §8(d):
+    node visits x 32 B + triangle tests x 64 B + top-level object tests x 128 B per cast."""
+    if kname.startswith("k_shadow"):
+        n = counts["shadow_casts"]
+        b = counts["shadow_node_visits"] * 32 + counts["shadow_tri_tests"] * 64 + counts["shadow_object_tests"] * 128
+        return n, (b / n if n else 0.0), "shadow cast"
+    if kname.startswith("k_extend"):
+        n = counts["casts"] - counts["shadow_casts"]
+        b = ((counts["node_visits"] - counts["shadow_node_visits"]) * 32 +
+             (counts["tri_tests"] - counts["shadow_tri_tests"]) * 64 +
+             (counts["object_tests"] - counts["shadow_object_tests"]) * 128)
+        return n, (b / n if n else 0.0), "closest-hit cast"
+    return None, None, None
 
 
 def cpu_baseline(blob, W, H, spp, kind, depth, target_s=12.0):
     """The oracle (C port of the reference path) timed on a bounded column subsample of the same frame."""
     from oracle import pyoracle
     threads = min(16, os.cpu_count() or 1)
-    # probe: a thin slice to estimate speed, then size the sample to ~target_s
-    stride = max(1, W // max(threads, 1))
+    stride = max(1, W // max(threads, 1))  # probe: a thin slice to estimate speed, then size the sample
     t = time.time()
     _, _, st = pyoracle.render(blob, W, H, spp, depth, kind, 1, 0, stride, threads=threads)
     dt = max(time.time() - t, 1e-3)
-    rate = st["samples"] / dt
-    want = rate * target_s
-    per_col = H * spp
-    ncols = int(max(threads, min(W, want / per_col)))
+    want = st["samples"] / dt * target_s
+    ncols = int(max(threads, min(W, want / (H * spp))))
     stride = max(1, W // ncols)
     t = time.time()
     _, _, st = pyoracle.render(blob, W, H, spp, depth, kind, 1, 0, stride, threads=threads)
@@ -70,13 +87,54 @@ def cpu_baseline(blob, W, H, spp, kind, depth, target_s=12.0):
             "sample": sample}, counts
 
 
-def load_pmc(config):
+def load_pmc(config, kname):
+    """Counters of kernel `kname` (any template instance: one kernel profile runs per scene)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
-    return d.get(config)
+        return None, None, kname
+    d = json.load(open(p)).get(config)
+    if not d:
+        return None, None, kname
+    hits = [k for k in d["kernels"] if k == kname or k.startswith(kname + "<")]
+    if len(hits) != 1:
+        return None, None, kname
+    return d["kernels"][hits[0]], d.get("source"), hits[0]
+
+
+def roofline(config, stats_ms, stats_launches, counts, samples_per_frame):
+    dom = max(stats_ms, key=lambda k: stats_ms[k])
+    kname = dom
+    launches = stats_launches[dom]
+    avg_ms = stats_ms[dom] / max(launches, 1)
+    per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
+    r = {"bound": "hbm", "kernel": kname, "unit": "GB/s", "peak": HBM_PEAK_GBS, "avg_launch_ms": avg_ms,
+         "launches_per_step": launches, "achieved": None, "frac": None, "traffic": None}
+    if per_sample:
+        units_per_launch = per_sample * samples_per_frame / launches
+        per_launch = bpu * units_per_launch
+        r.update(achieved=per_launch / (avg_ms * 1e-3) / 1e9, algorithmic_bytes_per_launch=per_launch,
+                 bytes_per_unit=bpu, work_unit=unit, units_per_launch=units_per_launch)
+        r["frac"] = r["achieved"] / HBM_PEAK_GBS
+    pmc, src, r["kernel"] = load_pmc(config, kname)
+    if pmc:
+        n = pmc["dispatches"]
+        traffic = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n  # KB -> B, gfx950 x2
+        r["traffic"] = traffic
+        r["traffic_GBs"] = traffic / (avg_ms * 1e-3) / 1e9
+        r["traffic_frac"] = r["traffic_GBs"] / HBM_PEAK_GBS
+        f64 = pmc.get("SQ_INSTS_VALU_ADD_F64", 0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0) + pmc.get("SQ_INSTS_VALU_FMA_F64", 0)
+        tr64, tr32 = pmc.get("SQ_INSTS_VALU_TRANS_F64", 0), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0)
+        other = pmc.get("SQ_INSTS_VALU", 0) - f64 - tr64 - tr32
+        lane = pmc["SQ_THREAD_CYCLES_VALU"] / (64 * pmc["SQ_ACTIVE_INST_VALU"]) if pmc.get("SQ_ACTIVE_INST_VALU") else None
+        issue = (f64 * ISSUE_CYC["f64"] + tr64 * ISSUE_CYC["trans_f64"] + tr32 * ISSUE_CYC["trans_f32"] +
+                 other * ISSUE_CYC["other"]) / n
+        flops = (pmc.get("SQ_INSTS_VALU_ADD_F64", 0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                 2 * pmc.get("SQ_INSTS_VALU_FMA_F64", 0)) * 64 * (lane or 1) / n
+        r["valu"] = {"issue_frac": issue / (SIMDS * CLOCK_HZ * avg_ms * 1e-3), "lane_utilisation": lane,
+                     "f64_tflops": flops / (avg_ms * 1e-3) / 1e12, "f64_peak_tflops": F64_PEAK_TFLOPS,
+                     "valu_insts_per_launch": pmc.get("SQ_INSTS_VALU", 0) / n}
+        r["pmc_source"] = src
+    return r
 
 
 def main():
@@ -98,6 +156,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import jsraytracer_amd as jr
+    from jsraytracer_amd.tiles import FrameGather
     from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline leg
 
     scene_name, W, H, spp, kind, depth = CONFIGS[args.config]
@@ -105,18 +164,14 @@ def main():
     scene = jr.Scene(blob, device=local)
 
     cb = args.col_block if world > 1 else 1
-    ncols = jr.owned_columns(W, rank, world, cb) if world > 1 else W
-    maxcols = max(jr.owned_columns(W, r, world, cb) for r in range(world)) if world > 1 else W
-    out = torch.zeros(maxcols * H, dtype=torch.int32, device=f"cuda:{local}")
-    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    fg = FrameGather(W, H, rank, world, cb, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
-        st = scene.render_device(out.data_ptr(), stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp,
+        st = scene.render_device(fg.local.data_ptr(), stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp,
                                  max_depth=depth, kind=kind, seed=1, x_offset=rank if world > 1 else 0,
                                  x_delt=world)
-        if world > 1:
-            dist.gather(out, gather, dst=0)
+        fg.gather()
         return st
 
     for _ in range(args.warmup):
@@ -137,11 +192,7 @@ def main():
 
     kernel_ms = sum(s["kernel_ms"] for s in stats) / len(stats)
     stage_ms = {k: sum(s["stage_ms"][k] for s in stats) / len(stats) for k in stats[0]["stage_ms"]}
-    stage_launches = stats[0]["stage_launches"]
-    kt = torch.tensor([kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-    kernel_ms = float(kt.item())
+    stage_launches = dict(stats[0]["stage_launches"])
 
     if rank == 0:
         total = W * H * spp
@@ -149,27 +200,21 @@ def main():
         cpu, counts = (None, None)
         if not args.no_cpu_baseline and world == 1:
             cpu, counts = cpu_baseline(blob, W, H, spp, kind, depth)
-        roof = None
-        if counts is not None:
-            bps = algorithmic_bytes_per_sample(counts, spp)
-            per_launch = bps * ncols * H * spp
-            achieved = per_launch / (kernel_ms * 1e-3) / 1e9
-            pmc = load_pmc(args.config)
-            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                    "bytes_per_sample": bps, "kernel_ms": kernel_ms,
-                    "counts_per_sample": {k: round(v, 4) for k, v in counts.items() if k != "samples"}}
+        roof = roofline(args.config, stage_ms, stage_launches, counts, fg.ncols * H * spp)
         line = {
             "metric": "pixel-samples/sec + %HBM-roofline, cornell_box_path 1024² @1/2/4/8 GPU",
             "value": value, "unit": "pixel-samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f64", "data": "reference scene graph (synthetic-free), keyed RNG seed 1",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "reference scene graph (exported from the live reference, not synthetic), keyed RNG seed 1",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth} (Incremental)", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"tiles{world}",
                        "col_block": cb},
             "roofline": roof, "cpu_baseline": cpu,
+            "kernel_ms_per_step": kernel_ms,
             "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
             "stage_launches_per_step": stage_launches,
+            "counts_per_sample": {k: round(v, 4) for k, v in counts.items() if k != "samples"} if counts else None,
         }
         print(json.dumps(line))
     if world > 1:

@@ -787,7 +787,16 @@ static Hit obj_intersect(Ctx *C, int o, Ray ray, double minD, double maxD, int s
 static Hit world_cast(Ctx *C, Ray ray, double minD, double maxD, int transp) { /* world.js:28-30 */
     C->st.casts++;
     C->st.object_tests += C->S->n_root;
-    return min_intersection(C, C->S->root, (int)C->S->n_root, ray, minD, maxD, transp);
+    if (transp) return min_intersection(C, C->S->root, (int)C->S->n_root, ray, minD, maxD, transp);
+    /* shadow cast (materials.js:250): its share of the counts, for per-kernel roofline figures */
+    const uint64_t nv = C->st.node_visits, tt = C->st.tri_tests, se = C->st.sdf_evals;
+    Hit h = min_intersection(C, C->S->root, (int)C->S->n_root, ray, minD, maxD, transp);
+    C->st.shadow_casts++;
+    C->st.shadow_object_tests += C->S->n_root;
+    C->st.shadow_node_visits += C->st.node_visits - nv;
+    C->st.shadow_tri_tests += C->st.tri_tests - tt;
+    C->st.shadow_sdf_evals += C->st.sdf_evals - se;
+    return h;
 }
 
 /* ---------------------------------- materials (materials.js) ------------------------------- */

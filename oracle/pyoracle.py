@@ -24,7 +24,8 @@ class OracleParams(ctypes.Structure):
                 ("pad", ctypes.c_int32)]
 
 
-STAT_FIELDS = ["samples", "color_calls", "casts", "object_tests", "node_visits", "tri_tests", "sdf_evals", "draws"]
+STAT_FIELDS = ["samples", "color_calls", "casts", "object_tests", "node_visits", "tri_tests", "sdf_evals", "draws",
+               "shadow_casts", "shadow_object_tests", "shadow_node_visits", "shadow_tri_tests", "shadow_sdf_evals"]
 
 
 class OracleStats(ctypes.Structure):

@@ -1,0 +1,77 @@
+"""N>1 path on CPU: world_size 2 and 3 gloo process groups running the bench's tile sharding
+(jsraytracer_amd/tiles.py) — column blocks per rank, one gather to rank 0, permute to image order.
+
+Each rank's tile is the oracle's render of exactly its owned columns (the oracle is the checker; on
+the GPU the tile comes from jsrt_render_device, whose block layout test_gpu_parity.py checks), so the
+composite must equal the single-process frame bit for bit, which in turn equals the reference's own
+x_delt=3 worker images (tests/golden, src/renderers.js:88)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, cb, tag, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from jsraytracer_amd.tiles import FrameGather, owned_px
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = pyoracle.golden_index()[tag]
+    blob = pyoracle.golden_scene(r["scene"])
+    # this rank's columns, rendered column by column in the reference's x_offset/x_delt form
+    # (a block of `cb` columns = cb interleave workers of stride W, one per column)
+    cols = owned_px(W, rank, world, cb)
+    fg = FrameGather(W, H, rank, world, cb)
+    tile = np.zeros((fg.maxcols, H), np.uint32)
+    for c, px in enumerate(cols):
+        _, rgba, _ = pyoracle.render(blob, W, H, r["spp"], r["depth"], r["kind"], r["seed"], int(px), W, threads=1)
+        tile[c] = rgba[:, px].view(np.uint32).reshape(H)
+    fg.local.copy_(torch.from_numpy(tile.view(np.int32).reshape(-1)))
+    img = fg.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "composite.npy"), FrameGather.to_rgba8(img))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 8), (3, 4), (3, 1)])
+def test_gloo_tile_gather_matches_reference(tmp_path, world, cb):
+    from oracle import pyoracle
+    tag = "cornell_box_path_incremental_32x32_s2_d8_seed5"
+    W = H = 32
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, cb, tag, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = np.load(tmp_path / "composite.npy")
+    _, grgba = pyoracle.golden_image(tag, W, H)
+    assert np.array_equal(got, grgba)
+
+
+def test_owned_columns_cover_the_frame_once():
+    from jsraytracer_amd import owned_columns
+    from jsraytracer_amd.tiles import column_permutation, max_owned, owned_px
+    for W in (1, 7, 32, 1000, 1024):
+        for world in (1, 2, 3, 8):
+            for cb in (1, 4, 16):
+                allc = np.concatenate([owned_px(W, r, world, cb) for r in range(world)])
+                assert sorted(allc.tolist()) == list(range(W))
+                for r in range(world):
+                    assert len(owned_px(W, r, world, cb)) == owned_columns(W, r, world, cb)
+                slot = column_permutation(W, world, cb)
+                assert len(set(slot.tolist())) == W and slot.max() < world * max_owned(W, world, cb)

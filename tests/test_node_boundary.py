@@ -1,0 +1,115 @@
+"""The Node side of the drop-in boundary: the N-API addon over libjsrt
+(jsraytracer_amd/js/jsrt_node.cpp) and the HipRenderer class keeping the reference's
+render(img, timelimit, callback, x_offset, x_delt) contract (src/renderers.js:10,70).
+
+CPU: the addon builds, loads in node, exports its functions, and fails loudly (a thrown Error with
+jsrt_last_error's message) without a device or with a bad blob.  GPU: node renders reference scenes
+through HipRenderer (sync, async, and the worker-protocol harness of src/worker.js) and the RGBA8
+bytes equal the reference-generated goldens."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JS = os.path.join(ROOT, "jsraytracer_amd", "js")
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+
+@pytest.fixture(scope="module")
+def addon():
+    from jsraytracer_amd import build as jb
+    jb.build()
+    subprocess.run(["sh", os.path.join(JS, "build_addon.sh")], check=True)
+    p = os.path.join(ROOT, "jsraytracer_amd", "_build", "jsrt_node.node")
+    assert os.path.exists(p)
+    return p
+
+
+def _node(code, timeout=120):
+    return subprocess.run([NODE, "-e", code], capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+def test_addon_exports(addon):
+    r = _node(f"const a=require({json.dumps(addon)}); console.log(JSON.stringify(Object.keys(a).sort()));"
+              "console.log(a.abiVersion(), a.ownedColumns(40,1,2,8), a.ownedColumns(10,1,3,1));")
+    assert r.returncode == 0, r.stderr
+    keys, nums = r.stdout.strip().split("\n")
+    assert json.loads(keys) == sorted(["sceneCreate", "sceneDestroy", "renderSync", "render", "deviceCount",
+                                       "abiVersion", "ownedColumns"])
+    assert nums.split() == ["1", "16", "3"]
+
+
+def test_addon_errors_are_thrown(addon):
+    r = _node(f"const a=require({json.dumps(addon)});"
+              "try {{ a.sceneCreate(new Uint8Array(10)); console.log('no throw'); }} catch (e) {{ console.log(e.message); }}"
+              .replace("{{", "{").replace("}}", "}"))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("jsrt_scene_create: ") and "no throw" not in r.stdout
+
+
+def test_hiprenderer_without_device_throws(addon):
+    from jsraytracer_amd import _native
+    if _native.lib().jsrt_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "ASimpleScene.jsrt.gz")
+    r = _node("const fs=require('fs'),z=require('zlib');const {HipRenderer}=require('./jsraytracer_amd/js/hip_renderer');"
+              f"const b=z.gunzipSync(fs.readFileSync({json.dumps(scene)}));"
+              "try { new HipRenderer(new Uint8Array(b)); console.log('no throw'); } catch (e) { console.log(e.message); }")
+    assert r.returncode == 0, r.stderr
+    assert "no throw" not in r.stdout and "jsrt_scene_create" in r.stdout
+
+
+def _render_cli(tmp_path, tag, mode="sync", xo=0, xd=1):
+    r = pyoracle.golden_index()[tag]
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", r["scene"] + ".jsrt.gz")
+    out = tmp_path / f"{tag}_{mode}_{xo}.rgba"
+    cmd = [NODE, os.path.join(JS, "render_cli.js"), scene, str(out)] + [
+        str(r[k]) for k in ("width", "height", "spp", "depth", "kind", "seed")] + [str(xo), str(xd), mode]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 0, p.stderr
+    return np.fromfile(out, np.uint8).reshape(r["height"], r["width"], 4), json.loads(p.stdout)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_node_hiprenderer_matches_reference(addon, tmp_path, mode):
+    tag = "ASimpleScene_incremental_64x64_s1_d4_seed1"
+    rgba, info = _render_cli(tmp_path, tag, mode)
+    r = pyoracle.golden_index()[tag]
+    _, grgba = pyoracle.golden_image(tag, r["width"], r["height"])
+    assert np.array_equal(rgba, grgba)
+    assert info["stats"]["samples"] == r["width"] * r["height"] * r["spp"]
+
+
+@pytest.mark.gpu
+def test_node_partition_matches_reference_workers(addon, tmp_path):
+    """x_offset/x_delt through the Node boundary equals the reference's own x_delt=3 worker images."""
+    full = "cornell_box_path_incremental_32x32_s2_d8_seed5"
+    for k in range(3):
+        rgba, _ = _render_cli(tmp_path, full, "sync", k, 3)
+        _, grgba = pyoracle.golden_image(full + f"_part{k}of3", 32, 32)
+        assert np.array_equal(rgba, grgba)
+
+
+@pytest.mark.gpu
+def test_node_worker_protocol_composite(addon, tmp_path):
+    """worker_harness.js: N worker_threads speaking src/worker.js's protocol, composited like
+    raytrace_launcher.js:92-97, equal the single-renderer image (partition invariance)."""
+    tag = "cornell_box_path_incremental_32x32_s2_d8_seed5"
+    r = pyoracle.golden_index()[tag]
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "cornell_box_path.jsrt.gz")
+    out = tmp_path / "composite.rgba"
+    p = subprocess.run([NODE, os.path.join(JS, "worker_harness.js"), scene, "3", str(out), "32", "32", "2", "5"],
+                       capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert p.returncode == 0, p.stderr
+    got = np.fromfile(out, np.uint8).reshape(32, 32, 4)
+    _, grgba = pyoracle.golden_image(tag, 32, 32)
+    assert r["depth"] == 8
+    assert np.array_equal(got, grgba)

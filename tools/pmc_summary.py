@@ -1,5 +1,10 @@
 """Summarise rocprofv3 --pmc csv passes per render kernel (k_gen, k_extend<PF>, k_shade<PF>, ...):
-counter sums over all dispatches of that kernel, plus derived per-wave figures."""
+counter sums over all dispatches of that kernel, plus derived per-wave figures.
+
+    python tools/pmc_summary.py <pmc dir> [--config NAME --merge profiles/pmc_summary.json]
+
+--merge adds {NAME: {"kernels": {kernel: {counter: sum, "dispatches": n}}}} to the committed summary
+that bench.py reads for roofline.traffic and the VALU figures."""
 import csv
 import glob
 import json
@@ -35,6 +40,14 @@ for k in sorted(tot):
                 print(f"   {c + ' / wave (x4 cyc)':28s} {4 * t[c] / w:.5g}")
     if t.get("SQ_THREAD_CYCLES_VALU") and t.get("SQ_ACTIVE_INST_VALU"):
         print(f"   VALU lane utilisation        {t['SQ_THREAD_CYCLES_VALU'] / (64 * t['SQ_ACTIVE_INST_VALU']):.3f}")
-    out[k] = t
+    out[k] = dict(t)
+    out[k]["dispatches"] = max(len(v) for v in disp[k].values())
 with open(os.path.join(root, "summary.json"), "w") as f:
     json.dump(out, f, indent=1)
+if "--merge" in sys.argv:
+    cfg = sys.argv[sys.argv.index("--config") + 1]
+    dst = sys.argv[sys.argv.index("--merge") + 1]
+    allp = json.load(open(dst)) if os.path.exists(dst) else {}
+    allp[cfg] = {"source": os.path.relpath(root) + " (rocprofv3 --pmc passes, bench.py --steps 1 --warmup 0)", "steps": 1, "kernels": out}
+    with open(dst, "w") as f:
+        json.dump(allp, f, indent=1, sort_keys=True)
