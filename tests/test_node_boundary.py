@@ -113,3 +113,26 @@ def test_node_worker_protocol_composite(addon, tmp_path):
     _, grgba = pyoracle.golden_image(tag, 32, 32)
     assert r["depth"] == 8
     assert np.array_equal(got, grgba)
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/math.js"), reason="reference sources absent (GPU box)")
+def test_live_scene_graph_export_matches_committed_blob(addon):
+    """HipRenderer(test.renderer) exports the LIVE reference scene graph (configureTest of
+    tests/cornell_box_path/test.mjs) to the same blob the GPU tests render; it then fails only for
+    want of a device here."""
+    code = ("const {loadScene}=require('./oracle/refharness/load_reference.js');"
+            "const {HipRenderer}=require('./jsraytracer_amd/js/hip_renderer.js');"
+            "const {exportScene}=require('./jsraytracer_amd/js/scene_blob.js');"
+            "const z=require('zlib'),fs=require('fs');"
+            "loadScene('cornell_box_path').then(t=>{const b=exportScene(t);"
+            "const g=z.gunzipSync(fs.readFileSync('tests/golden/scenes/cornell_box_path.jsrt.gz'));"
+            "console.log(Buffer.compare(Buffer.from(b),g)===0?'same':'differs');"
+            "try{new HipRenderer(t.renderer,{width:t.width,height:t.height});console.log('created')}"
+            "catch(e){console.log(e.message.split(':')[0])}});")
+    r = subprocess.run([NODE, "--experimental-modules", "-e", code], capture_output=True, text=True, timeout=120,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split()
+    assert lines[0] == "same"
+    from jsraytracer_amd import _native
+    assert lines[1] == ("created" if _native.lib().jsrt_device_count() > 0 else "jsrt_scene_create")
