@@ -125,10 +125,10 @@ def test_live_scene_graph_export_matches_committed_blob(addon):
             "const {exportScene}=require('./jsraytracer_amd/js/scene_blob.js');"
             "const z=require('zlib'),fs=require('fs');"
             "loadScene('cornell_box_path').then(t=>{const b=exportScene(t);"
-            "const g=z.gunzipSync(fs.readFileSync('tests/golden/scenes/cornell_box_path.jsrt.gz'));"
+            f"const g=z.gunzipSync(fs.readFileSync({json.dumps(os.path.join(ROOT, 'tests/golden/scenes/cornell_box_path.jsrt.gz'))}));"
             "console.log(Buffer.compare(Buffer.from(b),g)===0?'same':'differs');"
             "try{new HipRenderer(t.renderer,{width:t.width,height:t.height});console.log('created')}"
-            "catch(e){console.log(e.message.split(':')[0])}});")
+            "catch(e){console.log(e.message.split(':')[0])}}).catch(e=>{console.error(e);process.exit(1)});")
     r = subprocess.run([NODE, "--experimental-modules", "-e", code], capture_output=True, text=True, timeout=120,
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr
