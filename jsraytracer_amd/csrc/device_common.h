@@ -479,6 +479,10 @@ struct Hit {
     int ctx;
 };
 
+#ifdef JSRT_DBG_COUNT  // A/B instrumentation only: per-object lane / wave test counts of world_cast
+__device__ unsigned long long g_dbg[256];
+#endif
+
 template <int PF>
 __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DPrim &P, F3 o, F3 d, double minD,
                                                        double maxD) {
@@ -518,12 +522,36 @@ __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DP
     }
 }
 
-// Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
+// one row of Mat x Vec (math.js:392-397), the same operations as xf_point / xf_dir
+__device__ __forceinline__ float xf_row_point(const double *r, F3 o) {
+    return (float)((((double)o.x * r[0] + (double)o.y * r[1]) + (double)o.z * r[2]) + r[3]);
+}
+__device__ __forceinline__ float xf_row_dir(const double *r, F3 d) {
+    return (float)(((double)d.x * r[0] + (double)d.y * r[1]) + (double)d.z * r[2]);
+}
+
+// Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast.
+// `lim` = the caller's acceptance bound min(best, maxD): every caller accepts a distance only when
+// minD < t < lim, so a planar primitive whose plane distance already fails that test may return it
+// without transforming the x/y rows or testing its bounds; the caller's decision is unchanged.
 template <int PF>
 __device__ __forceinline__ double prim_intersect(const DScene &S, int pi, F3 o, F3 d, double minD, double maxD,
-                                                 bool transp) {
+                                                 bool transp, double lim) {
     const DPrim &P = S.prims[pi];
     if (!transp && !P.casts_shadow) return DINF;
+    const int k = P.gkind;
+    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) {
+        // SimplePlane.intersect (geometry.js:246-248) needs only the local z row
+        const float oz = xf_row_point(P.inv + 8, o), dz = xf_row_dir(P.inv + 8, d);
+        const double t = (dz != 0.0f) ? -(double)oz / (double)dz : -DINF;
+        if (k == JSRT_GEOM_PLANE || !(t > minD && t < lim)) return t;
+        const float ox = xf_row_point(P.inv, o), oy = xf_row_point(P.inv + 4, o);
+        const float dx = xf_row_dir(P.inv, d), dy = xf_row_dir(P.inv + 4, d);
+        const F3 p = ray_point(f3(ox, oy, oz), f3(dx, dy, dz), t);
+        if (k == JSRT_GEOM_SQUARE)  // geometry.js:287-291
+            return (-0.5f <= p.x && p.x <= 0.5f && -0.5f <= p.y && p.y <= 0.5f) ? t : -DINF;
+        return (dot3(p, p) <= 1) ? t : -DINF;  // Circle, geometry.js:310-314
+    }
     return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
 }
 
@@ -545,7 +573,7 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                 for (int k = 0; k < cnt; ++k) {
                     double t;
                     if (fast) t = tri_intersect(S.tris[S.leaf_tris[N.a + k]], o, d);
-                    else t = prim_intersect<PF>(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp);
+                    else t = prim_intersect<PF>(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp, fmin(maxD, best.t));
                     if (t > minD && t < maxD && t < best.t) {
                         best.t = t;
                         best.prim = S.leaf_prims[N.a + k];
@@ -591,7 +619,7 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
         const int c = S.inst_child[I.first + f.next++];
         const DInst &C = S.insts[c];
         if (C.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, C.prim, f.o, f.d, minD, maxD, transp);
+            const double t = prim_intersect<PF>(S, C.prim, f.o, f.d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, C.prim, I.ctx};
                 if (ANY) return;
@@ -619,6 +647,13 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     const float fminD = (float)minD;
     bool live = true;
+#ifdef JSRT_DBG_COUNT
+    const uint64_t act0 = __ballot(1);
+    if (__lane_id() == __builtin_ctzll(act0)) {
+        atomicAdd(&g_dbg[(ANY ? 128 : 0) + 126], (unsigned long long)__popcll(act0));
+        atomicAdd(&g_dbg[(ANY ? 128 : 0) + 127], 1ull);
+    }
+#endif
     for (int i = 0; i < S.n_roots; ++i) {
         const RootBound &RB = S.rbounds[i];
         bool need = live;
@@ -638,11 +673,20 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
             need = need && (tn <= tf) && (tf >= fminD) && (tn <= lim);
         }
         if (!__any(need)) continue;
+#ifdef JSRT_DBG_COUNT
+        {
+          const uint64_t act = __ballot(1), nb = __ballot(need);
+          if (__lane_id() == __builtin_ctzll(act)) {
+            atomicAdd(&g_dbg[(ANY ? 128 : 0) + 2 * i], (unsigned long long)__popcll(nb));
+            atomicAdd(&g_dbg[(ANY ? 128 : 0) + 2 * i + 1], 1ull);
+          }
+        }
+#endif
         if (!need) continue;
         const int ri = S.roots[i];
         const DInst &I = S.insts[ri];
         if (I.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, I.prim, o, d, minD, maxD, transp);
+            const double t = prim_intersect<PF>(S, I.prim, o, d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, I.prim, 0};
                 if (ANY) live = false;
@@ -672,8 +716,11 @@ __device__ __forceinline__ F3 mc_eval(const DScene &S, int m, float u, float v) 
     auto step = [&](int x) {  // next record below x (checkerboards resolved by (u, v))
         const jsrt_rec_mcolor &M = S.mc[x];
         if (M.kind == JSRT_MC_CHECKER) {  // materials.js:72-75
-            const double r = js_fmod(floor((double)u) + floor((double)v), 2);
-            return (fmod(r, 2.0) < 1) ? M.a : M.b;
+            // Math.fmod(a, 2) % 2 < 1 for a = floor(u) + floor(v): a is integral (or +-inf/NaN), so
+            // a - floor(a / 2) * 2 is exactly 0, 1 or NaN, on which toPrecision(8) and % 2 are the identity
+            const double a = floor((double)u) + floor((double)v);
+            const double r = a - floor(a / 2) * 2;
+            return (r < 1) ? M.a : M.b;
         }
         return M.a;
     };

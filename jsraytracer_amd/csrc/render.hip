@@ -448,7 +448,11 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) void k_shadow(DScene S, WArgs
     Rng rng{W.key[i], W.addr[i], (uint32_t)S.sample_call[s]};
     F3 delta, L, lcol;
     light_sample(S, Lt, P, rng, delta, L, lcol);
+#ifdef JSRT_AB_NOCAST
+    const Hit sh{DINF, -1, 0};
+#else
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
+#endif
     F3 c = f3(0, 0, 0);
     if (!(sh.prim >= 0 && sh.t > 0 && sh.t < 1)) {
         ShadeData sd;
@@ -460,7 +464,11 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) void k_shadow(DScene S, WArgs
         sd.kr = W.fkr[tt];
         const jsrt_rec_material &M = S.mat[W.fmat[tt]];
         sd.smoothness = M.smoothness;
+#ifdef JSRT_AB_NOCOLOR
+        c = lcol;
+#else
         c = light_sample_color((int)M.kind, sd, L, lcol);
+#endif
     }
     W.scx[e] = c.x;
     W.scy[e] = c.y;
@@ -758,5 +766,14 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     if (kt) kt->ev[KT_FINAL].end(st);
     return hipGetLastError();
 }
+
+#ifdef JSRT_DBG_COUNT
+extern "C" int jsrt_debug_counters(unsigned long long *out, int n) {
+    if (n > 256) n = 256;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long zero[256] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace jsrt
