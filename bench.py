@@ -101,11 +101,10 @@ def load_pmc(config, kname):
     return d["kernels"][hits[0]], d.get("source"), hits[0]
 
 
-def roofline(config, stats_ms, stats_launches, counts, samples_per_frame):
-    dom = max(stats_ms, key=lambda k: stats_ms[k])
+def roofline(config, dom, avg_ms, launches, counts, samples_per_frame):
+    """dom: the dominant kernel; avg_ms: its average launch duration from the HIP events that
+    bracketed its launches in the timed region (on the render stream)."""
     kname = dom
-    launches = stats_launches[dom]
-    avg_ms = stats_ms[dom] / max(launches, 1)
     per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
     r = {"bound": "hbm", "kernel": kname, "unit": "GB/s", "peak": HBM_PEAK_GBS, "avg_launch_ms": avg_ms,
          "launches_per_step": launches, "achieved": None, "frac": None, "traffic": None}
@@ -145,6 +144,7 @@ def main():
     ap.add_argument("--config", default="cornell_box_path", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--col-block", type=int, default=16)
+    ap.add_argument("--no-events", action="store_true", help="A/B: time steps without per-launch HIP events")
     args = ap.parse_args()
 
     rank, world, local = env_int("RANK", 0), env_int("WORLD_SIZE", 1), env_int("LOCAL_RANK", 0)
@@ -167,20 +167,28 @@ def main():
     fg = FrameGather(W, H, rank, world, cb, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step():
+    STAGES = jr._native.STAGES
+
+    def step(events=None):
+        """events: None = no HIP events; 0 = every stage; else a bitmask of stages (jsrt.h stage_events)."""
         st = scene.render_device(fg.local.data_ptr(), stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp,
                                  max_depth=depth, kind=kind, seed=1, x_offset=rank if world > 1 else 0,
-                                 x_delt=world)
+                                 x_delt=world, stats=events is not None, stage_events=events or 0)
         fg.gather()
         return st
 
-    for _ in range(args.warmup):
-        step()
+    # warmup; the last warmup step is fully instrumented and names the dominant kernel
+    st_full = None
+    for w in range(max(args.warmup, 1)):
+        st_full = step(0 if w == max(args.warmup, 1) - 1 else None)
+    dom = max(st_full["stage_ms"], key=lambda k: st_full["stage_ms"][k])
+    # timed region: HIP events bracket only the dominant kernel's launches (its average launch
+    # duration for the roofline); events on every launch would add launch gaps to the step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
+    stats = [step(None if args.no_events else (1 << STAGES.index(dom))) for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -189,10 +197,13 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
-
-    kernel_ms = sum(s["kernel_ms"] for s in stats) / len(stats)
-    stage_ms = {k: sum(s["stage_ms"][k] for s in stats) / len(stats) for k in stats[0]["stage_ms"]}
-    stage_launches = dict(stats[0]["stage_launches"])
+    if args.no_events:
+        stats = [step(1 << STAGES.index(dom))]
+    dom_ms = sum(s["stage_ms"][dom] for s in stats) / len(stats)
+    dom_launches = stats[0]["stage_launches"][dom]
+    # per-stage split: one more step after the timed region with every launch bracketed
+    st_after = step(0)
+    stage_ms, stage_launches, kernel_ms = st_after["stage_ms"], st_after["stage_launches"], st_after["kernel_ms"]
 
     if rank == 0:
         total = W * H * spp
@@ -200,7 +211,7 @@ def main():
         cpu, counts = (None, None)
         if not args.no_cpu_baseline and world == 1:
             cpu, counts = cpu_baseline(blob, W, H, spp, kind, depth)
-        roof = roofline(args.config, stage_ms, stage_launches, counts, fg.ncols * H * spp)
+        roof = roofline(args.config, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp)
         line = {
             "metric": "pixel-samples/sec + %HBM-roofline, cornell_box_path 1024² @1/2/4/8 GPU",
             "value": value, "unit": "pixel-samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -212,6 +223,7 @@ def main():
                        "col_block": cb},
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms_per_step": kernel_ms,
+            "stages_note": "stage split from one fully-instrumented step after the timed region",
             "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
             "stage_launches_per_step": stage_launches,
             "counts_per_sample": {k: round(v, 4) for k, v in counts.items() if k != "samples"} if counts else None,

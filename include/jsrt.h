@@ -43,7 +43,9 @@ typedef struct {
     int32_t samples_per_launch; /* progress granularity: samples per pixel between callbacks (<=0: all) */
     double timelimit_ms;     /* progress callback cadence (renderers.js:28-37); 0 = no callback */
     int32_t max_paths;       /* wavefront batch size in paths (<= 0: library default) */
-    int32_t reserved[5];
+    int32_t stage_events;    /* with stats: bitmask of the stages whose launches are bracketed by HIP
+                                events (bit k -> stage_ms[k]); 0 = all.  Events cost launch gaps. */
+    int32_t reserved[4];
 } jsrt_params;
 
 #define JSRT_STAGES 8
@@ -53,7 +55,7 @@ typedef struct {
     uint64_t samples;        /* pixel-samples rendered */
     uint32_t launches;       /* render-kernel launches */
     uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
-    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, lightsum */
+    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, resolve */
     uint32_t stage_launches[JSRT_STAGES];
 } jsrt_stats;
 

@@ -20,10 +20,10 @@ class Params(ctypes.Structure):
                 ("max_depth", ctypes.c_int32), ("kind", ctypes.c_int32), ("seed", ctypes.c_uint32),
                 ("x_offset", ctypes.c_int32), ("x_delt", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("samples_per_launch", ctypes.c_int32), ("timelimit_ms", ctypes.c_double),
-                ("max_paths", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
+                ("max_paths", ctypes.c_int32), ("stage_events", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
-STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_lightsum"]
+STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve"]
 
 
 class Stats(ctypes.Structure):

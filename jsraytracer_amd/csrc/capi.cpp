@@ -131,6 +131,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.sample_light = (const int32_t *)(b + o_sl);
     D.sample_call = (const int32_t *)(b + o_sc);
     D.light_draws = H.light_draws;
+    D.max_children = H.max_children;
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);
@@ -216,6 +217,7 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
         wf = own.get();
     }
     KernelTimes kt;
+    if (p && p->stage_events) kt.mask = (uint32_t)p->stage_events;
     auto t_last = std::chrono::steady_clock::now();
     const double tl = p ? p->timelimit_ms : 0;
     std::function<bool(int, double)> prog;
@@ -246,7 +248,7 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
         }
         st->kernel_ms = ms;
         st->launches = launches;
-        st->batches = (uint32_t)kt.ev[KT_ACCUM].used;
+        st->batches = kt.batches;
         st->samples = (uint64_t)a.ncols * a.H * a.spp;
     }
     (void)hipFreeAsync(accum, stream);

@@ -37,6 +37,9 @@ __device__ __forceinline__ double js_sign(double x) {
     return x > 0 ? 1.0 : -1.0;
 }
 __device__ __forceinline__ double js_pow(double x, double y) {
+#ifdef JSRT_AB_NOPOW  // A/B timing only: not the reference's arithmetic
+    return x * y;
+#endif
     if (is_nan(y)) return __builtin_nan("");
     if (y == 0.0) return 1.0;
     if ((x == 1.0 || x == -1.0) && __builtin_isinf(y)) return __builtin_nan("");
@@ -848,9 +851,15 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
     if (probSum == 0) return false;
     if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
         const double theta = 2.0 * JS_PI * rng.next();
+#ifdef JSRT_AB_NOTRIG  // A/B timing only: not the reference's arithmetic
+        const double phi = 2.0 * rng.next() - 1.0;
+        const double sin_phi = phi * 0.5;
+        const F3 sp3 = f3((float)(theta * sin_phi), or0((float)phi), or0((float)(theta * 0.1 * sin_phi)));
+#else
         const double phi = acos(2.0 * rng.next() - 1.0);
         const double sin_phi = sin(phi);
         const F3 sp3 = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
+#endif
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;

@@ -133,7 +133,8 @@ struct DScene {
     const int32_t *sample_light;  // per light sample s of a node (lights in order): its light
     const int32_t *sample_call;   // ... and the RNG call index of its first draw
     int32_t light_draws;     // RNG draws of all light samples of a node (scatter draws follow)
-    int32_t pad[3];
+    int32_t max_children;    // most children one ray-tree node can spawn (0..2)
+    int32_t pad[2];
 };
 
 }  // namespace jsrt

@@ -36,13 +36,25 @@
 #ifndef JSRT_EXTEND_OCC
 #define JSRT_EXTEND_OCC 1
 #endif
+// optional waves-per-EU window (min, max) per kernel for A/B occupancy experiments
+#ifdef JSRT_SHADOW_WPE
+#define SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(JSRT_SHADOW_WPE)))
+#else
+#define SHADOW_ATTR
+#endif
+#ifdef JSRT_SHADE_WPE
+#define SHADE_ATTR __attribute__((amdgpu_waves_per_eu(JSRT_SHADE_WPE)))
+#else
+#define SHADE_ATTR
+#endif
 
 namespace jsrt {
 
 const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final",
-                                    "k_lightsum"};
+                                    "k_resolve"};
 constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;  // camera ray: its result is the path's root colour
 constexpr uint32_t DEAD_RAY = 0xFFFFFFFEu;   // level-0 slot of a path outside the image (no result)
+constexpr int32_t NO_RAY = -2;                // W.prim of a slot that holds no ray to trace
 
 // block-aggregated append (one atomic per block: same-address atomics serialise device-wide).
 // Every thread of the block must call it.
@@ -69,13 +81,17 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
-__device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {
+__device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
     if (p == DEAD_RAY) return;
-    float *dst = (p == NO_PARENT) ? W.root + 3 * (size_t)W.path[i] : W.slot + 3 * (size_t)p;
-    dst[0] = c.x;
-    dst[1] = c.y;
-    dst[2] = c.z;
+    if (p == NO_PARENT) {
+        float *dst = W.root + 3 * (size_t)W.path[i];
+        dst[0] = c.x;
+        dst[1] = c.y;
+        dst[2] = c.z;
+    } else {
+        W.slot[(size_t)(p & 1u) * W.nstride + (p >> 1)] = make_float4(c.x, c.y, c.z, 0.0f);
+    }
 }
 
 // patch-ordered owned pixel index -> (owned column c, row py, image column px)
@@ -93,12 +109,39 @@ __device__ __forceinline__ Child pick(bool f, const Child &a, const Child &b) {
     return Child{pick(f, a.dir, b.dir), pick(f, a.col, b.col), pick(f, a.w, b.w), f ? a.k : b.k};
 }
 
+// Tree schedule: level L of the batch occupies pool slots [base, base + count).  Counts live on
+// the device (k_gen writes level 0, k_shade appends level L + 1), so the host enqueues every level
+// without reading them back; an overflowed batch reads as empty everywhere and is redone.
+struct LevelRange {
+    uint32_t base, count;
+};
+__device__ __forceinline__ LevelRange level_range(const WArgs &W, int L) {
+    if (W.lvl[LVL_FLAG]) return LevelRange{0u, 0u};
+    uint32_t b = 0;
+    for (int j = 0; j < L; ++j) b += W.lvl[j];
+    return LevelRange{b, W.lvl[L]};
+}
+
+// The material data k_shade hands to k_shadow for one lit node (after getBaseFactors), plus the
+// node's RNG frame (its light-sample draws come first, materials.js:244-257).
+struct Handoff {
+    F3 pos, N, R, refr, diff, spec;
+    double kr, smoothness;
+    int32_t mkind;
+    uint32_t addr, key;
+};
+struct NodeOut {
+    F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
+    uint32_t info;  // INFO_* bits + child count
+    Handoff h;      // h.pos (the hit point) is set for every hit; the rest for lit nodes
+};
+
 // World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
-// Geometry.materialData + Material.color (materials.js).  Writes the node (info, ambient / surface,
+// Geometry.materialData + Material.color (materials.js).  Fills the node (info, ambient / surface,
 // shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
 template <int PF>
-__device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint32_t i, uint32_t tt, const Hit &h, F3 o, F3 d,
-                          uint32_t addr, uint32_t key, Child &ch0, Child &ch1, F3 &pos) {
+__device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
+                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1) {
     const DPrim &P = S.prims[h.prim];
     // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409); the host
     // precomputed it (same operations) for identity prims and for the top-level context
@@ -222,21 +265,21 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
     }
     ShadeData sd;
     sd.pos = ray_point(o, d, h.t);  // material_data.position = ray.getPoint(distance)
-    pos = sd.pos;
+    out.h.pos = sd.pos;
+    out.h.addr = addr;
+    out.h.key = key;
     const jsrt_rec_material &M = S.mat[P.material];
     const int mkind = (int)M.kind;
     Rng rng{key, addr, 0};
     if (mkind == JSRT_MAT_SOLID) {
-        const F3 c = mc_eval(S, M.color, u, v);
-        W.sx[i] = c.x; W.sy[i] = c.y; W.sz[i] = c.z;
-        W.info[i] = INFO_HIT;
+        out.surf = mc_eval(S, M.color, u, v);
+        out.info = INFO_HIT;
         return 0;
     }
     if (mkind == JSRT_MAT_TRANSPARENT) {  // materials.js:169-173
-        const F3 a = scale(mc_eval(S, M.color, u, v), M.opacity);
-        W.sx[i] = a.x; W.sy[i] = a.y; W.sz[i] = a.z;
+        out.surf = scale(mc_eval(S, M.color, u, v), M.opacity);
         ch0 = Child{d, f3(1, 1, 1), f3(1, 1, 1), 1 - M.opacity};
-        W.info[i] = INFO_HIT | (1u << INFO_NCHILD_SHIFT);
+        out.info = INFO_HIT | (1u << INFO_NCHILD_SHIFT);
         return 1;
     }
     // getBaseFactors (materials.js:210-238)
@@ -288,18 +331,18 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
     // colorFromLights (materials.js:240-259): k_shadow evaluates the light samples (one lane each,
     // RNG calls [0, light_draws) of this frame) from the material data handed off here; the
     // scatter draws below follow them (calls light_draws, ...)
-    W.sx[i] = sd.ambient.x; W.sy[i] = sd.ambient.y; W.sz[i] = sd.ambient.z;
+    out.surf = sd.ambient;
     uint32_t info = INFO_HIT;
-    if (W.ns > 0) {
+    if (lit) {
         info |= INFO_LIT;
-        W.sox[tt] = sd.pos.x; W.soy[tt] = sd.pos.y; W.soz[tt] = sd.pos.z;
-        W.fnx[tt] = sd.N.x; W.fny[tt] = sd.N.y; W.fnz[tt] = sd.N.z;
-        W.frx[tt] = sd.R.x; W.fry[tt] = sd.R.y; W.frz[tt] = sd.R.z;
-        W.ftx[tt] = sd.refr.x; W.fty[tt] = sd.refr.y; W.ftz[tt] = sd.refr.z;
-        W.fdx[tt] = sd.diff.x; W.fdy[tt] = sd.diff.y; W.fdz[tt] = sd.diff.z;
-        W.fsx[tt] = sd.spec.x; W.fsy[tt] = sd.spec.y; W.fsz[tt] = sd.spec.z;
-        W.fkr[tt] = sd.kr;
-        W.fmat[tt] = P.material;
+        out.h.N = sd.N;
+        out.h.R = sd.R;
+        out.h.refr = sd.refr;
+        out.h.diff = sd.diff;
+        out.h.spec = sd.spec;
+        out.h.kr = sd.kr;
+        out.h.mkind = mkind;
+        out.h.smoothness = M.smoothness;
         rng.calls = (uint32_t)S.light_draws;
     }
     int n = 0;
@@ -326,27 +369,69 @@ __device__ __forceinline__ int shade_node(const DScene &S, const WArgs &W, uint3
             if (ok) push(Child{dir, col, sd.trans, 1 - sd.kr});
         }
     }
-    W.info[i] = info | ((uint32_t)n << INFO_NCHILD_SHIFT);
+    out.info = info | ((uint32_t)n << INFO_NCHILD_SHIFT);
     return n;
 }
 
 // ---------------------------------------------------------------------------------------------
+// Node / hand-off storage (AoS float4 records: one or two 16-B accesses per lane)
+__device__ __forceinline__ float u2f(uint32_t x) { return __uint_as_float(x); }
+__device__ __forceinline__ uint32_t f2u(float x) { return __float_as_uint(x); }
+
+__device__ __forceinline__ void store_node(const WArgs &W, uint32_t i, F3 c, uint32_t info) {
+    W.node[i] = make_float4(c.x, c.y, c.z, u2f(info));
+}
+__device__ __forceinline__ void store_child(const WArgs &W, uint32_t i, uint32_t j, const Child &c) {
+    float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
+    x[0] = make_float4(c.col.x, c.col.y, c.col.z, c.w.x);
+    x[W.nstride] = make_float4(c.w.y, c.w.z, u2f((uint32_t)__double2loint(c.k)), u2f((uint32_t)__double2hiint(c.k)));
+}
+// ((v * col) * w) * k added to c: surface.plus(child.times(col).times(w).times(k)) (materials.js:277-330)
+__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v) {
+    const float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
+    const float4 a = x[0], b = x[W.nstride];
+    const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
+    return add(c, scale(mul(mul(v, f3(a.x, a.y, a.z)), f3(a.w, b.x, b.y)), k));
+}
+__device__ __forceinline__ void store_hand(const WArgs &W, uint32_t h, const Handoff &o) {
+    float4 *p = W.hand + h;
+    const size_t hs = W.hstride;
+    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f((uint32_t)o.mkind));
+    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f((uint32_t)__double2loint(o.kr)));
+    p[2 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f((uint32_t)__double2hiint(o.kr)));
+    p[3 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f(o.addr));
+    p[4 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(o.key));
+    p[5 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2loint(o.smoothness)));
+    p[6 * hs] = make_float4(u2f((uint32_t)__double2hiint(o.smoothness)), 0.0f, 0.0f, 0.0f);
+}
+
+// per pixel, the renderer's f32 accumulation of one sample (renderers.js:93-97, 52-61)
+__device__ __forceinline__ F3 accumulate(const RenderArgs &A, F3 acc, F3 col) {
+    if (A.kind == JSRT_RENDERER_RANDOM) return add(acc, scale(col, 1.0 / A.spp));
+    if (A.kind == JSRT_RENDERER_INCREMENTAL) return f3(acc.x + col.x, acc.y + or0(col.y), acc.z + or0(col.z));  // buffer.plus(c.to4(true))
+    return col;
+}
+
+// ---------------------------------------------------------------------------------------------
+// camera rays: one per path q of the batch, sample-major (neighbouring q are neighbouring pixels)
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
-    // level 0 holds one camera ray per path of the batch at slot q (no append); paths whose pixel
-    // lies outside the image (edge patches) get a DEAD_RAY slot that misses and writes nothing
-    const uint32_t q = blockIdx.x * 256 + threadIdx.x;  // path index in the batch
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (!W.chain && q < 64) W.lvl[q] = q == 0 ? W.npaths : 0u;  // level counts and overflow flag
     if (q >= W.npaths) return;
     int c = 0, py = 0, px = 0;
-    const uint32_t pl = q % W.npix, sl = q / W.npix;  // sample-major: neighbours are neighbour pixels
+    const uint32_t pl = q % W.npix, sl = q / W.npix;
     const uint32_t smp = W.s0 + sl;
     const bool valid = pixel_of(A, W.p0 + pl, c, py, px);
-    if (A.max_depth <= 0) {  // World.color(ray, 0) = black; no level is traced
-        W.root[3 * q] = W.root[3 * q + 1] = W.root[3 * q + 2] = 0.0f;
-        return;
+    if (!W.chain) {
+        if (A.max_depth <= 0) {  // World.color(ray, 0) = black; no level is traced
+            W.root[3 * q] = W.root[3 * q + 1] = W.root[3 * q + 2] = 0.0f;
+            return;
+        }
+        W.path[q] = q;
+        W.parent[q] = valid ? NO_PARENT : DEAD_RAY;
     }
-    W.path[q] = q;
-    if (!valid) {
-        W.parent[q] = DEAD_RAY;
+    if (!valid || A.max_depth <= 0) {  // edge patch outside the image: no ray
+        W.prim[q] = NO_RAY;
         return;
     }
     const uint32_t pixel = (uint32_t)(py * A.W + px);
@@ -365,18 +450,22 @@ __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     W.dx[q] = d.x; W.dy[q] = d.y; W.dz[q] = d.z;
     W.addr[q] = mix32(0u, 1u);
     W.key[q] = key;
-    W.parent[q] = NO_PARENT;
+    W.prim[q] = -1;
 }
 
-template <int PF>
-__global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, uint32_t base, uint32_t count, double minD) {
+// Closest hit (World.cast, world.js:28-30).  Chain: ray q of the batch; tree: level L's range.
+template <int PF, bool CHAIN>
+__global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L, double minD) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= count) return;
-    const uint32_t i = base + t;
-    if (W.parent[i] == DEAD_RAY) {
-        W.prim[i] = -1;
-        return;
+    uint32_t i = t;
+    if (CHAIN) {
+        if (t >= W.npaths) return;
+    } else {
+        const LevelRange R = level_range(W, L);
+        if (t >= R.count) return;
+        i = R.base + t;
     }
+    if (W.prim[i] == NO_RAY) return;
     const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
     const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
     W.t[i] = h.t;
@@ -384,141 +473,199 @@ __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs
     W.ctx[i] = h.ctx;
 }
 
-template <int PF>
-__global__ __launch_bounds__(256, JSRT_SHADE_OCC) void k_shade(DScene S, WArgs W, uint32_t base, uint32_t count, int child_depth) {
-    const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
+// World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
+// Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
+// Tree schedule: node = pool slot; children are appended to level L + 1 (block-aggregated).
+template <int PF, bool CHAIN>
+__global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene S, WArgs W, int L, int child_depth) {
+    const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
+    uint32_t count = W.npaths, base = 0, next_base = 0;
+    if (!CHAIN) {
+        const LevelRange R = level_range(W, L);
+        count = R.count;
+        base = R.base;
+        next_base = R.base + R.count;
+        if (t0 >= count) return;  // block-uniform: every thread of a live block reaches block_append
+    } else if (tt >= count) {
+        return;
+    }
     const bool in = tt < count;
-    const uint32_t i = base + (in ? tt : 0u);
+    const uint32_t q = in ? tt : 0u;                                     // ray slot (chain) / level index (tree)
+    const uint32_t i = CHAIN ? (uint32_t)L * W.npaths + q : base + q;    // node index
+    const uint32_t r = CHAIN ? q : i;                                    // ray index
     int nchild = 0;
     Child ch0, ch1;
-    F3 pos = f3(0, 0, 0);
-    uint32_t addr = 0, key = 0;
+    NodeOut out;
     bool hit = false;
-    if (in) {
-        const int prim = W.prim[i];
-        if (prim < 0) {  // miss: World.color returns bg_color (world.js:35-36)
-            write_result(W, i, f3(S.bg[0], S.bg[1], S.bg[2]));
-            W.info[i] = 0;
+    const int prim = in ? W.prim[r] : NO_RAY;
+    if (prim == NO_RAY) {
+        if (in) store_node(W, i, f3(0, 0, 0), 0u);
+    } else if (prim < 0) {  // miss: World.color returns bg_color (world.js:35-36)
+        const F3 bg = f3(S.bg[0], S.bg[1], S.bg[2]);
+        if (CHAIN) {
+            store_node(W, i, bg, INFO_MISS);
+            W.prim[r] = NO_RAY;
         } else {
-            hit = true;
-            const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
-            addr = W.addr[i];
-            key = W.key[i];
-            const Hit h{W.t[i], prim, W.ctx[i]};
-            nchild = shade_node<PF>(S, W, i, tt, h, o, d, addr, key, ch0, ch1, pos);
+            write_result(W, i, bg);
+            store_node(W, i, bg, 0u);
         }
+    } else {
+        hit = true;
+        const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
+        const Hit h{W.t[r], prim, W.ctx[r]};
+        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
+        store_node(W, i, out.surf, out.info);
+        if (out.info & INFO_LIT) store_hand(W, q, out.h);
+        if (nchild > 0) store_child(W, i, 0, ch0);
+        if (nchild > 1) store_child(W, i, 1, ch1);
     }
-    // children: World.color(child, depth - 1); at depth 0 they are black without a cast
-    const uint32_t at = block_append<256>(W.counter, child_depth > 0 ? nchild : 0);
-    if (!hit) return;
-    const uint32_t path = W.path[i];
-    auto emit = [&](const Child &c, uint32_t j) {
-        const uint32_t sl = 2 * i + j;
-        W.ccol[3 * sl] = c.col.x; W.ccol[3 * sl + 1] = c.col.y; W.ccol[3 * sl + 2] = c.col.z;
-        W.cw[3 * sl] = c.w.x; W.cw[3 * sl + 1] = c.w.y; W.cw[3 * sl + 2] = c.w.z;
-        W.ck[sl] = c.k;
-        if (child_depth > 0) {
-            const uint32_t r = at + j;
-            W.ox[r] = pos.x; W.oy[r] = pos.y; W.oz[r] = pos.z;
-            W.dx[r] = c.dir.x; W.dy[r] = c.dir.y; W.dz[r] = c.dir.z;
-            W.addr[r] = mix32(addr, j + 1);
-            W.key[r] = key;
-            W.path[r] = path;
-            W.parent[r] = sl;
+    if (CHAIN) {  // the child ray (World.color(child, depth - 1)) takes over slot q
+        if (!hit) return;
+        if (child_depth > 0 && nchild > 0) {
+            W.ox[r] = out.h.pos.x; W.oy[r] = out.h.pos.y; W.oz[r] = out.h.pos.z;
+            W.dx[r] = ch0.dir.x; W.dy[r] = ch0.dir.y; W.dz[r] = ch0.dir.z;
+            W.addr[r] = mix32(out.h.addr, 1u);
         } else {
-            W.slot[3 * sl] = W.slot[3 * sl + 1] = W.slot[3 * sl + 2] = 0.0f;
+            W.prim[r] = NO_RAY;  // no child, or children black without a cast (depth 0)
         }
-    };
-    if (nchild > 0) emit(ch0, 0);
-    if (nchild > 1) emit(ch1, 1);
+        return;
+    }
+    // tree: children append to level L + 1; at depth 0 they are black without a cast
+    const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
+    if (!hit || nchild == 0) return;
+    if (child_depth == 0) {
+        W.slot[i] = make_float4(0, 0, 0, 0);
+        if (nchild > 1) W.slot[W.nstride + i] = make_float4(0, 0, 0, 0);
+        return;
+    }
+    if ((size_t)at + nchild > W.level_cap || (size_t)next_base + at + nchild > W.pool) {
+        W.lvl[LVL_FLAG] = 1u;  // overflow: the host redoes the batch smaller
+        return;
+    }
+    const uint32_t path = W.path[r];
+    for (int j = 0; j < nchild; ++j) {
+        const Child &c = j == 0 ? ch0 : ch1;
+        const uint32_t rr = next_base + at + (uint32_t)j;
+        W.ox[rr] = out.h.pos.x; W.oy[rr] = out.h.pos.y; W.oz[rr] = out.h.pos.z;
+        W.dx[rr] = c.dir.x; W.dy[rr] = c.dir.y; W.dz[rr] = c.dir.z;
+        W.addr[rr] = mix32(out.h.addr, (uint32_t)j + 1);
+        W.key[rr] = out.h.key;
+        W.path[rr] = path;
+        W.parent[rr] = 2 * i + (uint32_t)j;
+        W.prim[rr] = -1;
+    }
 }
 
-// One light sample of a lit node per lane (lane e = level index * ns + sample): the sample
-// (lights.js sampleIterator), its shadow cast (materials.js:250-252) and, when unshadowed,
-// colorFromLightSample (materials.js:261-269, 340-356); shadowed samples contribute 0.
+// The light samples of the lit nodes of level L (lights.js sampleIterator), their shadow casts
+// (materials.js:250-252), colorFromLightSample (materials.js:261-269, 340-356) and the
+// colorFromLights sums (materials.js:244-257), which turn the node's ambient into its surface.
+// W.group lanes serve one node (sample s on lane s, a power of two >= ns); the node's first lane
+// adds the samples in the reference's order from its neighbours' registers.  SERIAL (more than 64
+// samples per node, group 1): one lane per node walks all samples itself.
 template <int PF>
-__global__ __launch_bounds__(256, JSRT_SHADOW_OCC) void k_shadow(DScene S, WArgs W, uint32_t base, uint32_t count) {
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t ns = (uint32_t)W.ns;
-    if (e >= count * ns) return;
-    const uint32_t tt = e / ns, s = e - tt * ns, i = base + tt;
-    if (!(W.info[i] & INFO_LIT)) return;
-    const F3 P = f3(W.sox[tt], W.soy[tt], W.soz[tt]);
-    const DLight &Lt = S.lights[S.sample_light[s]];
-    Rng rng{W.key[i], W.addr[i], (uint32_t)S.sample_call[s]};
+__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s) {
+    const float4 h0 = hp[0];
+    const F3 P = f3(h0.x, h0.y, h0.z);
+    Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
     F3 delta, L, lcol;
-    light_sample(S, Lt, P, rng, delta, L, lcol);
+#ifdef JSRT_LIGHT_UNIFORM  // one light: its record (and colour chain) through scalar loads
+    if (S.n_lights == 1) light_sample(S, S.lights[0], P, rng, delta, L, lcol);
+    else
+#endif
+    light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
 #ifdef JSRT_AB_NOCAST
     const Hit sh{DINF, -1, 0};
 #else
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
 #endif
-    F3 c = f3(0, 0, 0);
-    if (!(sh.prim >= 0 && sh.t > 0 && sh.t < 1)) {
-        ShadeData sd;
-        sd.N = f3(W.fnx[tt], W.fny[tt], W.fnz[tt]);
-        sd.R = f3(W.frx[tt], W.fry[tt], W.frz[tt]);
-        sd.refr = f3(W.ftx[tt], W.fty[tt], W.ftz[tt]);
-        sd.diff = f3(W.fdx[tt], W.fdy[tt], W.fdz[tt]);
-        sd.spec = f3(W.fsx[tt], W.fsy[tt], W.fsz[tt]);
-        sd.kr = W.fkr[tt];
-        const jsrt_rec_material &M = S.mat[W.fmat[tt]];
-        sd.smoothness = M.smoothness;
+    if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) return f3(0, 0, 0);  // shadowed: contributes +0
+    const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
+    ShadeData sd;
+    sd.N = f3(h1.x, h1.y, h1.z);
+    sd.R = f3(h2.x, h2.y, h2.z);
+    sd.refr = f3(h3.x, h3.y, h3.z);
+    sd.diff = f3(h4.x, h4.y, h4.z);
+    sd.spec = f3(h5.x, h5.y, h5.z);
+    sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
+    sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
 #ifdef JSRT_AB_NOCOLOR
-        c = lcol;
+    return lcol;
 #else
-        c = light_sample_color((int)M.kind, sd, L, lcol);
+    return light_sample_color((int)f2u(h0.w), sd, L, lcol);
 #endif
-    }
-    W.scx[e] = c.x;
-    W.scy[e] = c.y;
-    W.scz[e] = c.z;
 }
 
-// colorFromLights' sums (materials.js:244-257): per light, its samples in order (a shadowed
-// sample adds +0, which never changes an f32 running sum that starts at +0), times 1/samples.
-__global__ __launch_bounds__(256) void k_lightsum(DScene S, WArgs W, uint32_t base, uint32_t count) {
-    const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
-    if (tt >= count) return;
-    const uint32_t i = base + tt;
-    if (!(W.info[i] & INFO_LIT)) return;
-    F3 ret = f3(W.sx[i], W.sy[i], W.sz[i]);  // ambient
-    size_t e = (size_t)tt * W.ns;
+template <int PF, bool CHAIN, bool SERIAL>
+__global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DScene S, WArgs W, int L) {
+    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
+    if (!CHAIN) {
+        const LevelRange R = level_range(W, L);
+        count = R.count;
+        base = R.base;
+    }
+    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t q = e / G, s = e % G;  // G is a power of two
+    const bool in = q < count;
+    const uint32_t i = base + (in ? q : 0u);
+    const float4 nd = W.node[i];
+    const bool lit = in && (f2u(nd.w) & INFO_LIT);
+    const float4 *hp = W.hand + (in ? q : 0u);
+    F3 ret = f3(nd.x, nd.y, nd.z);  // ambient
+    if (SERIAL) {  // one lane per node: every sample in order
+        if (!lit) return;
+        uint32_t k = 0;
+        for (int li = 0; li < S.n_lights; ++li) {
+            const DLight &Lt = S.lights[li];
+            const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
+            F3 light_color = f3(0, 0, 0);
+            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k));
+            if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
+        }
+        W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
+        return;
+    }
+    F3 c = f3(0, 0, 0);
+    if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s);
+    // colorFromLights: per light, its samples in order (a shadowed sample adds +0, which never
+    // changes an f32 running sum that starts at +0), times 1/samples; every lane takes part
+    const int lane0 = (int)(__lane_id() & ~(G - 1));
+    uint32_t k = 0;
     for (int li = 0; li < S.n_lights; ++li) {
         const DLight &Lt = S.lights[li];
-        const int ns = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
+        const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
         F3 light_color = f3(0, 0, 0);
-        for (int k = 0; k < ns; ++k, ++e) light_color = add(light_color, f3(W.scx[e], W.scy[e], W.scz[e]));
-        if (ns > 0) ret = add(ret, scale(light_color, 1.0 / ns));
+        for (int j = 0; j < n; ++j, ++k) {
+            const int src = lane0 + (int)k;
+            light_color = add(light_color, f3(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src)));
+        }
+        if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
     }
-    W.sx[i] = ret.x;
-    W.sy[i] = ret.y;
-    W.sz[i] = ret.z;
+    if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
 
-// surface.plus(child.times(col).times(w).times(k)) for the children in order (materials.js:277-330)
-__global__ __launch_bounds__(256) void k_reduce(WArgs W, uint32_t base, uint32_t count) {
+// tree schedule: surface + children, bottom-up into the parent's child slot (materials.js:277-330)
+__global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
+    const LevelRange R = level_range(W, L);
     const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
-    if (tt >= count) return;
-    const uint32_t i = base + tt;
-    const uint32_t info = W.info[i];
+    if (tt >= R.count) return;
+    const uint32_t i = R.base + tt;
+    const float4 nd = W.node[i];
+    const uint32_t info = f2u(nd.w);
     if (!(info & INFO_HIT)) return;
-    F3 c = f3(W.sx[i], W.sy[i], W.sz[i]);
+    F3 c = f3(nd.x, nd.y, nd.z);
     const int n = (int)((info >> INFO_NCHILD_SHIFT) & 3);
     for (int j = 0; j < n; ++j) {
-        const uint32_t sl = 2 * i + (uint32_t)j;
-        const F3 v = f3(W.slot[3 * sl], W.slot[3 * sl + 1], W.slot[3 * sl + 2]);
-        const F3 col = f3(W.ccol[3 * sl], W.ccol[3 * sl + 1], W.ccol[3 * sl + 2]);
-        const F3 w = f3(W.cw[3 * sl], W.cw[3 * sl + 1], W.cw[3 * sl + 2]);
-        c = add(c, scale(mul(mul(v, col), w), W.ck[sl]));
+        const float4 v = W.slot[(size_t)j * W.nstride + i];
+        c = add_child(W, i, (uint32_t)j, c, f3(v.x, v.y, v.z));
     }
     write_result(W, i, c);
 }
 
-// per pixel, the batch's samples in order (renderers.js:93-97, 52-61)
+// tree schedule: per pixel, the batch's samples in order
 __global__ __launch_bounds__(256) void k_accum(RenderArgs A, WArgs W) {
     const uint32_t pl = blockIdx.x * 256 + threadIdx.x;
-    if (pl >= W.npix) return;
+    if (pl >= W.npix || W.lvl[LVL_FLAG]) return;  // an overflowed batch is redone by the host
     int c, py, px;
     if (!pixel_of(A, W.p0 + pl, c, py, px)) return;
     const size_t oi = (size_t)c * A.H + py;
@@ -526,11 +673,39 @@ __global__ __launch_bounds__(256) void k_accum(RenderArgs A, WArgs W) {
     const uint32_t nsb = W.npaths / W.npix;
     for (uint32_t sl = 0; sl < nsb; ++sl) {
         const uint32_t q = sl * W.npix + pl;
-        const F3 col = f3(W.root[3 * q], W.root[3 * q + 1], W.root[3 * q + 2]);
-        if (A.kind == JSRT_RENDERER_RANDOM) acc = add(acc, scale(col, 1.0 / A.spp));
-        else if (A.kind == JSRT_RENDERER_INCREMENTAL)
-            acc = f3(acc.x + col.x, acc.y + or0(col.y), acc.z + or0(col.z));  // buffer.plus(c.to4(true))
-        else acc = col;
+        acc = accumulate(A, acc, f3(W.root[3 * q], W.root[3 * q + 1], W.root[3 * q + 2]));
+    }
+    A.accum[4 * oi] = acc.x;
+    A.accum[4 * oi + 1] = acc.y;
+    A.accum[4 * oi + 2] = acc.z;
+}
+
+// chain schedule: per pixel, its samples in order; each path's colour is resolved bottom-up over
+// its levels (surface + child contribution; a last-level child is black without a cast)
+__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
+    const uint32_t pl = blockIdx.x * 256 + threadIdx.x;
+    if (pl >= W.npix) return;
+    int c, py, px;
+    if (!pixel_of(A, W.p0 + pl, c, py, px)) return;
+    const size_t oi = (size_t)c * A.H + py;
+    F3 acc = f3(A.accum[4 * oi], A.accum[4 * oi + 1], A.accum[4 * oi + 2]);
+    const uint32_t nsb = W.npaths / W.npix, P = W.npaths;
+    for (uint32_t sl = 0; sl < nsb; ++sl) {
+        const uint32_t q = sl * W.npix + pl;
+        F3 v = f3(0, 0, 0);  // World.color(ray, 0) = black
+        for (int L = A.max_depth - 1; L >= 0; --L) {
+            const uint32_t i = (uint32_t)L * P + q;
+            const float4 nd = W.node[i];
+            const uint32_t info = f2u(nd.w);
+            if (info & INFO_MISS) {
+                v = f3(nd.x, nd.y, nd.z);
+            } else if (info & INFO_HIT) {
+                F3 col = f3(nd.x, nd.y, nd.z);
+                if ((info >> INFO_NCHILD_SHIFT) & 3) col = add_child(W, i, 0, col, L == A.max_depth - 1 ? f3(0, 0, 0) : v);
+                v = col;
+            }
+        }
+        acc = accumulate(A, acc, v);
     }
     A.accum[4 * oi] = acc.x;
     A.accum[4 * oi + 1] = acc.y;
@@ -589,46 +764,37 @@ EventPairs::~EventPairs() {
     for (auto x : e) (void)hipEventDestroy(x);
 }
 
-hipError_t Wavefront::reserve(size_t pool, size_t level_cap, int ns) {
-    if (mem && pool <= cap_pool && level_cap <= cap_level && ns <= cap_ns) return hipSuccess;
+hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree) {
     size_t bytes = 0;
-    bytes += 10 * need(pool, 4) + need(pool, 8) + 2 * need(pool, 4);  // rays + hits
-    bytes += 4 * need(pool, 4);                                      // info + surface
-    bytes += 3 * need(6 * pool, 4) + need(2 * pool, 8);              // ccol cw slot + ck
-    bytes += 18 * need(level_cap, 4) + need(level_cap, 8) + need(level_cap, 4) + 3 * need(level_cap * (size_t)ns, 4);
-    bytes += need(3 * level_cap, 4) + 256;
-    if (mem) (void)hipFree(mem);
-    mem = nullptr;
-    cap_pool = cap_level = 0;
-    hipError_t e = hipMalloc(&mem, bytes);
-    if (e != hipSuccess) return e;
-    cap_bytes = bytes;
-    cap_pool = pool;
-    cap_level = level_cap;
-    cap_ns = ns;
+    bytes += 8 * need(rays, 4) + need(rays, 8) + 2 * need(rays, 4);  // o d addr key + t + prim ctx
+    if (tree) bytes += 2 * need(rays, 4);                            // path parent
+    bytes += need(nodes, 16) + need(4 * nodes, 16);                  // node + child
+    if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
+    bytes += need(7 * hands, 16) + need(64, 4);                      // hand-off + level counts
+    if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
+    } else {
+        if (mem) (void)hipFree(mem);
+        mem = nullptr;
+        cap_bytes = 0;
+        hipError_t e = hipMalloc(&mem, bytes);
+        if (e != hipSuccess) return e;
+        cap_bytes = bytes;
+    }
     uint8_t *p = static_cast<uint8_t *>(mem);
     WArgs &w = args;
-    w.ox = carve<float>(p, pool); w.oy = carve<float>(p, pool); w.oz = carve<float>(p, pool);
-    w.dx = carve<float>(p, pool); w.dy = carve<float>(p, pool); w.dz = carve<float>(p, pool);
-    w.addr = carve<uint32_t>(p, pool); w.key = carve<uint32_t>(p, pool);
-    w.path = carve<uint32_t>(p, pool); w.parent = carve<uint32_t>(p, pool);
-    w.t = carve<double>(p, pool); w.prim = carve<int32_t>(p, pool); w.ctx = carve<int32_t>(p, pool);
-    w.info = carve<uint32_t>(p, pool);
-    w.sx = carve<float>(p, pool); w.sy = carve<float>(p, pool); w.sz = carve<float>(p, pool);
-    w.ccol = carve<float>(p, 6 * pool); w.cw = carve<float>(p, 6 * pool); w.slot = carve<float>(p, 6 * pool);
-    w.ck = carve<double>(p, 2 * pool);
-    w.sox = carve<float>(p, level_cap); w.soy = carve<float>(p, level_cap); w.soz = carve<float>(p, level_cap);
-    w.fnx = carve<float>(p, level_cap); w.fny = carve<float>(p, level_cap); w.fnz = carve<float>(p, level_cap);
-    w.frx = carve<float>(p, level_cap); w.fry = carve<float>(p, level_cap); w.frz = carve<float>(p, level_cap);
-    w.ftx = carve<float>(p, level_cap); w.fty = carve<float>(p, level_cap); w.ftz = carve<float>(p, level_cap);
-    w.fdx = carve<float>(p, level_cap); w.fdy = carve<float>(p, level_cap); w.fdz = carve<float>(p, level_cap);
-    w.fsx = carve<float>(p, level_cap); w.fsy = carve<float>(p, level_cap); w.fsz = carve<float>(p, level_cap);
-    w.fkr = carve<double>(p, level_cap);
-    w.fmat = carve<int32_t>(p, level_cap);
-    const size_t se = level_cap * (size_t)ns;
-    w.scx = carve<float>(p, se); w.scy = carve<float>(p, se); w.scz = carve<float>(p, se);
-    w.root = carve<float>(p, 3 * level_cap);
-    w.counter = carve<uint32_t>(p, 64);
+    w = WArgs{};
+    w.ox = carve<float>(p, rays); w.oy = carve<float>(p, rays); w.oz = carve<float>(p, rays);
+    w.dx = carve<float>(p, rays); w.dy = carve<float>(p, rays); w.dz = carve<float>(p, rays);
+    w.addr = carve<uint32_t>(p, rays); w.key = carve<uint32_t>(p, rays);
+    w.t = carve<double>(p, rays); w.prim = carve<int32_t>(p, rays); w.ctx = carve<int32_t>(p, rays);
+    if (tree) { w.path = carve<uint32_t>(p, rays); w.parent = carve<uint32_t>(p, rays); }
+    w.node = carve<float4>(p, nodes);
+    w.child = carve<float4>(p, 4 * nodes);
+    if (tree) { w.slot = carve<float4>(p, 2 * nodes); w.root = carve<float>(p, 3 * paths); }
+    w.hand = carve<float4>(p, 7 * hands);
+    w.lvl = carve<uint32_t>(p, 64);
+    w.nstride = nodes;
+    w.hstride = hands;
     return hipSuccess;
 }
 
@@ -637,56 +803,57 @@ Wavefront::~Wavefront() {
 }
 
 namespace {
-template <int PF>
-hipError_t run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
-                     uint32_t *h_counter, bool &overflow) {
+inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 255) / 256); }
+
+// Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.
+// Tree: each level's launch is sized by an upper bound of its ray count (the real count is on
+// the device and surplus blocks exit at once); levels are reduced bottom-up afterwards.
+template <int PF, bool CHAIN>
+void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt) {
     auto timed = [&](int which, auto launch) {
-        if (kt) kt->ev[which].begin(st);
+        const bool ev = kt && kt->on(which);
+        if (ev) kt->ev[which].begin(st);
         launch();
-        if (kt) kt->ev[which].end(st);
+        if (ev) kt->ev[which].end(st);
     };
-    std::vector<uint32_t> lvl_base, lvl_count;
-    overflow = false;
-    hipError_t e;
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
-    uint32_t base = 0, count = A.max_depth > 0 ? W.npaths : 0;
-    for (int L = 0; L < A.max_depth && count > 0; ++L) {
-        const uint32_t next = base + count;
+    std::vector<size_t> ubs;  // upper bound of each level's ray count
+    size_t ub = A.max_depth > 0 ? W.npaths : 0;
+    for (int L = 0; L < A.max_depth && ub > 0; ++L) {
+        ubs.push_back(ub);
         const int child_depth = A.max_depth - L - 1;
-        if ((size_t)count > W.level_cap || (child_depth > 0 && (size_t)next + 2 * (size_t)count > W.pool)) {
-            overflow = true;
-            return hipSuccess;
-        }
-        lvl_base.push_back(base);
-        lvl_count.push_back(count);
         timed(KT_EXTEND, [&] {
-            hipLaunchKernelGGL(k_extend<PF>, dim3(grid(count)), dim3(256), 0, st, S, W, base, count,
-                               L == 0 ? 0.0 : 0.0001);
+            hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
-        *h_counter = next;
-        if ((e = hipMemcpyAsync(W.counter, h_counter, 4, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
         timed(KT_SHADE, [&] {
-            hipLaunchKernelGGL(k_shade<PF>, dim3(grid(count)), dim3(256), 0, st, S, W, base, count, child_depth);
+            hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
         });
-        if (W.ns > 0) {
+        if (W.ns > 0)
             timed(KT_SHADOW, [&] {
-                hipLaunchKernelGGL(k_shadow<PF>, dim3(grid((size_t)count * W.ns)), dim3(256), 0, st, S, W, base, count);
+                if (W.ns <= 64)
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), 0, st, S, W, L);
+                else
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L);
             });
-            timed(KT_LIGHTSUM, [&] {
-                hipLaunchKernelGGL(k_lightsum, dim3(grid(count)), dim3(256), 0, st, S, W, base, count);
-            });
-        }
-        if ((e = hipMemcpyAsync(h_counter, W.counter, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        base = next;
-        count = *h_counter - next;
+        if (!CHAIN) ub = child_depth > 0 ? std::min(ub * (size_t)S.max_children, W.level_cap) : 0;
     }
-    for (int L = (int)lvl_base.size() - 1; L >= 0; --L)
-        timed(KT_REDUCE, [&] {
-            hipLaunchKernelGGL(k_reduce, dim3(grid(lvl_count[L])), dim3(256), 0, st, W, lvl_base[L], lvl_count[L]);
-        });
+    if (CHAIN) {
+        timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
+        return;
+    }
+    for (int L = (int)ubs.size() - 1; L >= 0; --L)
+        timed(KT_REDUCE, [&] { hipLaunchKernelGGL(k_reduce, dim3(grid_ub(ubs[L])), dim3(256), 0, st, W, L); });
     timed(KT_ACCUM, [&] { hipLaunchKernelGGL(k_accum, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
-    return hipGetLastError();
+}
+
+template <bool CHAIN>
+void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt) {
+    switch (S.profile) {
+    case PF_ANALYTIC: run_batch<PF_ANALYTIC, CHAIN>(S, A, W, st, kt); break;
+    case PF_MESH: run_batch<PF_MESH, CHAIN>(S, A, W, st, kt); break;
+    case PF_SDF: run_batch<PF_SDF, CHAIN>(S, A, W, st, kt); break;
+    default: run_batch<PF_ALL, CHAIN>(S, A, W, st, kt); break;
+    }
 }
 }  // namespace
 
@@ -699,24 +866,39 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     uint32_t npix = npix_total, nsb = 1;  // batch: [p0, p0 + npix) pixels x [s0, s0 + nsb) samples
     if ((size_t)npix > max_paths) npix = (uint32_t)(max_paths & ~(size_t)63);
     else nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)A.spp));
-    // ray pool for all levels of a batch; one level may hold up to half of it (Fresnel / glass
-    // materials spawn two children per hit).  A one-patch batch that still overflows grows it.
-    size_t pool = (size_t)npix * nsb * 8, level_cap = pool / 2;
-    hipError_t e = wf.reserve(pool, level_cap, ns > 0 ? ns : 1);
+    // Chain schedule when no node can have two children: depth x paths node records, no
+    // overflow possible, batches enqueued back to back.  Tree schedule otherwise: a ray pool for
+    // all levels of a batch (one level may hold half of it); each batch's overflow flag is read
+    // back and an overflowed batch is redone in halves (a one-patch batch grows the pool).
+    const bool chain = S.max_children <= 1;
+    const int depth = std::max(1, A.max_depth);
+    const size_t paths = (size_t)npix * nsb;
+    size_t pool = chain ? paths : paths * 8, level_cap = chain ? paths : pool / 2;
+    auto reserve = [&]() {
+        return chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false)
+                     : wf.reserve(pool, pool, level_cap, level_cap, true);
+    };
+    hipError_t e = reserve();
     if (e != hipSuccess) return e;
     WArgs W = wf.args;
-    W.ns = ns;
-    W.pool = pool;
-    W.level_cap = level_cap;
+    auto setup = [&](WArgs &w) {
+        w.ns = ns;
+        w.group = 1;
+        if (ns > 1 && ns <= 64)
+            while (w.group < ns) w.group *= 2;
+        w.chain = chain ? 1 : 0;
+        w.pool = pool;
+        w.level_cap = level_cap;
+    };
+    setup(W);
     if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) return e;
-    uint32_t *h_counter = nullptr;
-    if ((e = hipHostMalloc((void **)&h_counter, 16, 0)) != hipSuccess) return e;
+    uint32_t *h_flag = nullptr;  // overflow read-back (tree schedule only)
+    if (!chain && (e = hipHostMalloc((void **)&h_flag, 16, 0)) != hipSuccess) return e;
     const uint64_t total = (uint64_t)npix_total * A.spp;
     uint64_t done = 0;
     for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess; s0 += nsb) {
         const uint32_t nb = std::min<uint32_t>(nsb, (uint32_t)A.spp - s0);
         for (uint32_t p0 = 0; p0 < npix_total && e == hipSuccess; p0 += npix) {
-            // halve the pixel range until the batch fits (branching materials grow the levels)
             std::vector<std::pair<uint32_t, uint32_t>> todo{{p0, std::min(npix, npix_total - p0)}};
             while (!todo.empty() && e == hipSuccess) {
                 const auto job = todo.back();
@@ -725,45 +907,46 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 W.npix = job.second;
                 W.s0 = s0;
                 W.npaths = job.second * nb;
-                bool overflow = false;
-                switch (S.profile) {
-                case PF_ANALYTIC: e = run_batch<PF_ANALYTIC>(S, A, W, st, kt, h_counter, overflow); break;
-                case PF_MESH: e = run_batch<PF_MESH>(S, A, W, st, kt, h_counter, overflow); break;
-                case PF_SDF: e = run_batch<PF_SDF>(S, A, W, st, kt, h_counter, overflow); break;
-                default: e = run_batch<PF_ALL>(S, A, W, st, kt, h_counter, overflow); break;
-                }
-                if (e != hipSuccess) break;
-                if (overflow) {
-                    if (job.second <= 64) {  // cannot split further: grow the pool and retry
-                        if (pool > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
-                        if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                        pool *= 2;
-                        level_cap = pool / 2;
-                        if ((e = wf.reserve(pool, level_cap, ns > 0 ? ns : 1)) != hipSuccess) break;
-                        const WArgs keep = W;
-                        W = wf.args;
-                        W.ns = ns;
-                        W.pool = pool;
-                        W.level_cap = level_cap;
-                        W.p0 = keep.p0; W.npix = keep.npix; W.s0 = keep.s0; W.npaths = keep.npaths;
-                        todo.push_back(job);
+                if (chain) run_batch_pf<true>(S, A, W, st, kt);
+                else run_batch_pf<false>(S, A, W, st, kt);
+                if ((e = hipGetLastError()) != hipSuccess) break;
+                if (!chain) {  // k_accum skipped an overflowed batch; the host redoes it
+                    if ((e = hipMemcpyAsync(h_flag, W.lvl + LVL_FLAG, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+                    if (*h_flag) {
+                        if (job.second <= 64) {  // cannot split further: grow the pool and retry
+                            if (pool > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
+                            pool *= 2;
+                            level_cap = pool / 2;
+                            if ((e = reserve()) != hipSuccess) break;
+                            const WArgs keep = W;
+                            W = wf.args;
+                            setup(W);
+                            W.p0 = keep.p0; W.npix = keep.npix; W.s0 = keep.s0; W.npaths = keep.npaths;
+                            todo.push_back(job);
+                            continue;
+                        }
+                        const uint32_t half = ((job.second / 2) + 63) & ~63u;
+                        todo.push_back({job.first + half, job.second - half});
+                        todo.push_back({job.first, half});
                         continue;
                     }
-                    const uint32_t half = ((job.second / 2) + 63) & ~63u;
-                    todo.push_back({job.first + half, job.second - half});
-                    todo.push_back({job.first, half});
-                    continue;
                 }
                 done += (uint64_t)job.second * nb;
+                if (kt) ++kt->batches;
             }
         }
-        if (e == hipSuccess && progress && !progress((int)(s0 + nb - 1), (double)done / (double)total)) break;
+        if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+            if (!progress((int)(s0 + nb - 1), (double)done / (double)total)) break;
+        }
     }
-    (void)hipHostFree(h_counter);
+    if (h_flag) (void)hipHostFree(h_flag);  // its last read-back was synchronised
     if (e != hipSuccess) return e;
-    if (kt) kt->ev[KT_FINAL].begin(st);
+    const bool ev = kt && kt->on(KT_FINAL);
+    if (ev) kt->ev[KT_FINAL].begin(st);
     hipLaunchKernelGGL(k_final, dim3(grid((size_t)A.ncols * A.H)), dim3(256), 0, st, A);
-    if (kt) kt->ev[KT_FINAL].end(st);
+    if (ev) kt->ev[KT_FINAL].end(st);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 namespace jsrt {
 
 constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of the breadth-first schedule)
+constexpr int LVL_FLAG = 63;        // overflow flag slot of WArgs::lvl (64 words)
 
 struct RenderArgs {
     int32_t W, H, kind, max_depth;
@@ -26,55 +27,52 @@ struct RenderArgs {
     int32_t pad;
 };
 
-// node info bits (k_shade -> k_shadow / k_reduce)
-constexpr uint32_t INFO_HIT = 1u, INFO_LIT = 2u;
+// node info bits (k_shade -> k_shadow / k_reduce / k_resolve)
+constexpr uint32_t INFO_HIT = 1u, INFO_LIT = 2u, INFO_MISS = 16u;
 constexpr int INFO_NCHILD_SHIFT = 2;
 
-// Device buffers of one batch (structure of arrays over a ray pool shared by all levels).
+// Device buffers of one batch.  Two schedules share them (render.hip):
+//   chain (no node has more than one child): ray q of the batch is path q at every level; node
+//         records are level-major [L * npaths + q]; the child ray replaces its parent's ray.
+//   tree  (branching materials): rays and nodes share pool slots; level L occupies
+//         [base_L, base_L + count_L) with counts on the device; children are appended.
 struct WArgs {
-    // rays (index = pool slot); level L occupies [base_L, base_L + count_L)
+    // rays
     float *ox, *oy, *oz, *dx, *dy, *dz;
     uint32_t *addr;    // ray-tree address of the World.color frame this ray opens
     uint32_t *key;     // mix(mix(seed, pixel), sample): RNG key of the path
-    uint32_t *path;    // path index in the batch
-    uint32_t *parent;  // 2 * parent slot + child index, or NO_PARENT for camera rays
+    uint32_t *path;    // tree: path index in the batch
+    uint32_t *parent;  // tree: child slot 2 * parent + j, NO_PARENT (camera ray) or DEAD_RAY
     double *t;         // closest hit
-    int32_t *prim, *ctx;
-    // nodes (same index as the ray that reached them)
-    uint32_t *info;
-    float *sx, *sy, *sz;  // ambient, then resolved surface colour
-    float *ccol, *cw, *slot;  // [3 * (2 * i + j)]: child weights and child results
-    double *ck;               // [2 * i + j]
-    // shade -> shadow hand-off of one level (index = ray index within the level): the node's
-    // material_data after getBaseFactors, as colorFromLightSample reads it
-    float *sox, *soy, *soz;          // position (shadow-ray origin)
-    float *fnx, *fny, *fnz;          // N (flipped to the viewer's side)
-    float *frx, *fry, *frz;          // R
-    float *ftx, *fty, *ftz;          // refraction direction (0 when none)
-    float *fdx, *fdy, *fdz;          // diffuse colour (basecolor applied)
-    float *fsx, *fsy, *fsz;          // specular colour
-    double *fkr;                     // Fresnel reflection factor (1 for Phong)
-    int32_t *fmat;                   // material index
-    float *scx, *scy, *scz;          // [level_idx * ns + sample]: unshadowed sample colour or 0
-    float *root;       // [3 * path]
-    uint32_t *counter; // append counter of the next level
+    int32_t *prim, *ctx;  // prim: hit primitive, -1 miss / to trace, NO_RAY no ray
+    // nodes
+    float4 *node;      // [i]: {surface colour (the ambient until k_shadow adds the lights), info}
+    // record planes (plane stride nstride / hstride): every access is one coalesced 16-B load per lane
+    float4 *child;     // [(2 * j + part) * nstride + i]: part 0 {col.xyz, w.x}, part 1 {w.y, w.z, k (f64)}
+    float4 *slot;      // tree: [j * nstride + i] the child's colour
+    float4 *hand;      // [k * hstride + h], k < 7: shadow hand-off of a lit node (h: path / level index)
+    float *root;       // tree: [3 * path] root colours
+    uint32_t *lvl;     // tree: [L] ray count of level L; [LVL_FLAG] overflow flag
     // batch
     uint32_t p0, npix, s0, npaths;
     int32_t ns;        // light samples per lit node
-    uint32_t pad;
+    int32_t group;     // lanes per node in k_shadow: a power of two >= ns (<= 64), or 1 (serial)
+    int32_t chain;     // schedule
+    int32_t pad;
     size_t pool, level_cap;
+    size_t nstride, hstride;  // plane strides of child / slot and of hand
 };
 
 struct Wavefront {  // owns the batch buffers (cached per scene)
     void *mem = nullptr;
-    size_t cap_bytes = 0, cap_pool = 0, cap_level = 0;
-    int cap_ns = 0;
+    size_t cap_bytes = 0;
     WArgs args{};
-    hipError_t reserve(size_t pool, size_t level_cap, int ns);
+    // rays: ray slots; nodes: node records; hands: hand-off records; paths: root colours
+    hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree);
     ~Wavefront();
 };
 
-enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_LIGHTSUM, KT_N };
+enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_N };
 extern const char *const KT_NAMES[KT_N];
 
 struct EventPairs {  // reusable HIP events bracketing every launch of one kernel kind
@@ -88,6 +86,9 @@ struct EventPairs {  // reusable HIP events bracketing every launch of one kerne
 
 struct KernelTimes {
     EventPairs ev[KT_N];
+    uint32_t mask = ~0u;  // stages whose launches are bracketed by events
+    uint32_t batches = 0; // (pixels x samples) batches completed
+    bool on(int k) const { return (mask >> k) & 1u; }
     void reset() {
         for (auto &p : ev) p.used = 0;
     }

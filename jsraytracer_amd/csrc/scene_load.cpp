@@ -6,6 +6,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <unordered_map>
 
@@ -790,6 +791,33 @@ struct Loader {
             if (pr.gkind == JSRT_GEOM_TRIANGLE) f |= PF_TRI;
         }
         S.features = f;
+        // most children one ray-tree node can spawn (materials.js:277-330), conservatively: the
+        // wavefront pool is sized by it and a scene with <= 1 needs no per-batch overflow check
+        auto maybe_nonzero = [&](int32_t m) {  // could this colour chain evaluate to a non-zero vector?
+            std::vector<int32_t> todo{m};
+            for (int g = 0; g < 64 && !todo.empty(); ++g) {
+                const int32_t x = todo.back();
+                todo.pop_back();
+                if (x < 0) continue;
+                const jsrt_rec_mcolor &c = B.mc[x];
+                if (c.kind == JSRT_MC_SOLID) {
+                    for (uint32_t k = 0; k < c.len && k < 4; ++k)
+                        if (!(c.vec[k] == 0.0f)) return true;
+                } else if (c.kind == JSRT_MC_CHECKER) {
+                    todo.push_back(c.a);
+                    todo.push_back(c.b);
+                } else todo.push_back(c.a);
+            }
+            return !todo.empty();
+        };
+        S.max_children = 0;
+        for (const jsrt_rec_material &M : S.mat) {
+            int n = 0;
+            if (M.kind == JSRT_MAT_TRANSPARENT) n = 1;
+            else if (M.kind == JSRT_MAT_PHONG) n = (int)maybe_nonzero(M.reflect) + (int)maybe_nonzero(M.transmit);
+            else if (M.kind != JSRT_MAT_SOLID) n = isinf(M.ratio) ? 1 : 2;  // infinite ratio: kr = 1
+            S.max_children = std::max(S.max_children, n);
+        }
         shading_matrices();
         S.profile = f == 0 ? PF_ANALYTIC : (f & ~PF_MESH) == 0 ? PF_MESH : (f & ~PF_SDF) == 0 ? PF_SDF : PF_ALL;
         for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);

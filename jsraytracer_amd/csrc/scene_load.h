@@ -37,6 +37,7 @@ struct HostScene {
     float bg[4];
     int32_t kind, spp, max_depth, width, height;
     int32_t all_roots_prims;
+    int32_t max_children = 2;  // most children a ray-tree node can spawn (0..2)
     int32_t features = 0, profile = PF_ALL;  // PF_* bits used / kernel instantiation chosen
     // workload facts used for algorithmic-byte accounting
     int64_t n_bvh_nodes = 0, n_triangles = 0;

@@ -65,9 +65,9 @@ class Scene:
 
     @staticmethod
     def params(width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, device=0,
-               samples_per_launch=0, timelimit_ms=0.0, max_paths=0):
+               samples_per_launch=0, timelimit_ms=0.0, max_paths=0, stage_events=0):
         return Params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, device, samples_per_launch,
-                      timelimit_ms, max_paths)
+                      timelimit_ms, max_paths, stage_events)
 
     def render(self, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1,
                samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0, max_paths=0):
@@ -90,15 +90,16 @@ class Scene:
         check(rc, "jsrt_render")
         return rgba, colors, st.as_dict()
 
-    def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, **kw):
-        """Render owned columns into device buffers (see jsrt.h jsrt_render_device)."""
+    def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, stats=True, **kw):
+        """Render owned columns into device buffers (see jsrt.h jsrt_render_device).  stats=False
+        records no per-launch HIP events (and returns None)."""
         L = _native.lib()
         p = self.params(device=self.device, **kw)
-        st = Stats()
+        st = Stats() if stats else None
         rc = L.jsrt_render_device(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
-                                  ctypes.byref(st))
+                                  ctypes.byref(st) if stats else None)
         check(rc, "jsrt_render_device")
-        return st.as_dict()
+        return st.as_dict() if stats else None
 
     def header(self):
         return scene_header(self._blob)
