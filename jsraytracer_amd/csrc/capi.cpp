@@ -96,7 +96,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     sc->device = device;
     DeviceArena A;
     const size_t o_prims = A.add(H.prims), o_insts = A.add(H.insts), o_ichild = A.add(H.inst_child),
-                 o_roots = A.add(H.roots), o_rb = A.add(H.rbounds), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
+                 o_roots = A.add(H.roots), o_rb = A.add(H.rbounds), o_rr = A.add(H.rootrec), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
                  o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
                  o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_matf = A.add(H.mat_flags), o_ps = A.add(H.prim_shade),
                  o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
@@ -114,6 +114,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.inst_child = (const int32_t *)(b + o_ichild);
     D.roots = (const int32_t *)(b + o_roots);
     D.rbounds = (const RootBound *)(b + o_rb);
+    D.rootrec = (const DRoot *)(b + o_rr);
     D.mats = (const double *)(b + o_mats);
     D.ctx = (const double *)(b + o_ctx);
     D.bvh = (const DBvhNode *)(b + o_bvh);

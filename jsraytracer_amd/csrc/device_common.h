@@ -538,9 +538,8 @@ __device__ __forceinline__ float xf_row_dir(const double *r, F3 d) {
 // minD < t < lim, so a planar primitive whose plane distance already fails that test may return it
 // without transforming the x/y rows or testing its bounds; the caller's decision is unchanged.
 template <int PF>
-__device__ __forceinline__ double prim_intersect(const DScene &S, int pi, F3 o, F3 d, double minD, double maxD,
+__device__ __forceinline__ double prim_intersect(const DScene &S, const DPrim &P, F3 o, F3 d, double minD, double maxD,
                                                  bool transp, double lim) {
-    const DPrim &P = S.prims[pi];
     if (!transp && !P.casts_shadow) return DINF;
     const int k = P.gkind;
     if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) {
@@ -576,7 +575,7 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                 for (int k = 0; k < cnt; ++k) {
                     double t;
                     if (fast) t = tri_intersect(S.tris[S.leaf_tris[N.a + k]], o, d);
-                    else t = prim_intersect<PF>(S, S.leaf_prims[N.a + k], o, d, minD, maxD, transp, fmin(maxD, best.t));
+                    else t = prim_intersect<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp, fmin(maxD, best.t));
                     if (t > minD && t < maxD && t < best.t) {
                         best.t = t;
                         best.prim = S.leaf_prims[N.a + k];
@@ -622,7 +621,7 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
         const int c = S.inst_child[I.first + f.next++];
         const DInst &C = S.insts[c];
         if (C.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, C.prim, f.o, f.d, minD, maxD, transp, fmin(maxD, best.t));
+            const double t = prim_intersect<PF>(S, S.prims[C.prim], f.o, f.d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, C.prim, I.ctx};
                 if (ANY) return;
@@ -653,12 +652,13 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
 #ifdef JSRT_DBG_COUNT
     const uint64_t act0 = __ballot(1);
     if (__lane_id() == __builtin_ctzll(act0)) {
-        atomicAdd(&g_dbg[(ANY ? 128 : 0) + 126], (unsigned long long)__popcll(act0));
-        atomicAdd(&g_dbg[(ANY ? 128 : 0) + 127], 1ull);
+        atomicAdd(&g_dbg[(ANY ? 192 : 128) + 62], (unsigned long long)__popcll(act0));
+        atomicAdd(&g_dbg[(ANY ? 192 : 128) + 63], 1ull);
     }
 #endif
     for (int i = 0; i < S.n_roots; ++i) {
-        const RootBound &RB = S.rbounds[i];
+        const DRoot &R = S.rootrec[i];
+        const RootBound &RB = R.rb;
         bool need = live;
         if (RB.bounded) {
             const float e = RB.k * oabs + RB.e0;
@@ -680,31 +680,29 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         {
           const uint64_t act = __ballot(1), nb = __ballot(need);
           if (__lane_id() == __builtin_ctzll(act)) {
-            atomicAdd(&g_dbg[(ANY ? 128 : 0) + 2 * i], (unsigned long long)__popcll(nb));
-            atomicAdd(&g_dbg[(ANY ? 128 : 0) + 2 * i + 1], 1ull);
+            atomicAdd(&g_dbg[(ANY ? 192 : 128) + 2 * i], (unsigned long long)__popcll(nb));
+            atomicAdd(&g_dbg[(ANY ? 192 : 128) + 2 * i + 1], 1ull);
           }
         }
 #endif
         if (!need) continue;
-        const int ri = S.roots[i];
-        const DInst &I = S.insts[ri];
-        if (I.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, I.prim, o, d, minD, maxD, transp, fmin(maxD, best.t));
+        if (R.kind == INST_PRIM) {
+            const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
-                best = Hit{t, I.prim, 0};
+                best = Hit{t, R.prim, 0};
                 if (ANY) live = false;
             }
         } else if (!(PF & (PF_BVH | PF_AGG))) {
             continue;
-        } else if ((PF & PF_BVH) && I.kind == INST_BVH) {
-            const double *m = S.mats + 12 * I.matrix;
-            const Hit h = bvh_cast<PF, ANY>(S, I, xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
+        } else if ((PF & PF_BVH) && R.kind == INST_BVH) {
+            const double *m = R.p.inv;
+            const Hit h = bvh_cast<PF, ANY>(S, S.insts[R.inst], xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
                 if (ANY) live = false;
             }
         } else if (PF & PF_AGG) {
-            nested_cast<PF, ANY>(S, ri, o, d, minD, maxD, transp, best);
+            nested_cast<PF, ANY>(S, R.inst, o, d, minD, maxD, transp, best);
             if (ANY && best.prim >= 0) live = false;
         }
     }

@@ -57,6 +57,16 @@ struct RootBound {       // conservative world-space box of one top-level object
 };
 static_assert(sizeof(RootBound) == 48, "RootBound");
 
+struct DRoot {           // one top-level object flattened for the world loop: every field the cull
+    RootBound rb;        // and the test read sits in one record, read through independent scalar loads
+    int32_t kind;        // INST_*
+    int32_t inst;        // DInst index
+    int32_t prim;        // INST_PRIM: DPrim index (p is its copy); else -1
+    int32_t pad;
+    DPrim p;             // INST_PRIM: the primitive; AGG/BVH: p.inv = the object's inverse matrix
+};
+static_assert(sizeof(DRoot) == 208, "DRoot");
+
 struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
     float cx, cy, cz;
     int32_t a;           // internal: lesser child; leaf: first index into leaf_prims[]
@@ -105,6 +115,7 @@ struct DScene {
     const int32_t *inst_child;
     const int32_t *roots;
     const RootBound *rbounds;   // parallel to roots
+    const DRoot *rootrec;       // parallel to roots (world_cast)
     const double *mats;      // 12 doubles per AGG/BVH instance matrix
     const double *ctx;       // 16 doubles per shading context (ctx 0 = identity)
     const DBvhNode *bvh;

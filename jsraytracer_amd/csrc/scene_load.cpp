@@ -743,6 +743,18 @@ struct Loader {
             if (S.insts[ix].kind != INST_PRIM) S.all_roots_prims = 0;
         }
         root_bounds();
+        for (size_t i = 0; i < S.roots.size(); ++i) {
+            DRoot r;
+            memset(&r, 0, sizeof r);
+            const DInst &in = S.insts[S.roots[i]];
+            r.rb = S.rbounds[i];
+            r.kind = in.kind;
+            r.inst = S.roots[i];
+            r.prim = in.kind == INST_PRIM ? in.prim : -1;
+            if (in.kind == INST_PRIM) r.p = S.prims[in.prim];
+            else memcpy(r.p.inv, &S.mats[12 * (size_t)in.matrix], sizeof r.p.inv);
+            S.rootrec.push_back(r);
+        }
         for (uint32_t i = 0; i < B.n_lite; ++i) {
             const jsrt_rec_light &L = B.lite[i];
             DLight d;

@@ -14,6 +14,7 @@ struct HostScene {
     std::vector<DInst> insts;
     std::vector<int32_t> inst_child, roots;
     std::vector<RootBound> rbounds;
+    std::vector<DRoot> rootrec;
     std::vector<double> mats, ctx;
     std::vector<DBvhNode> bvh;
     std::vector<int32_t> leaf_prims, leaf_tris;
