@@ -57,6 +57,8 @@ typedef struct {
     uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
     double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, resolve */
     uint32_t stage_launches[JSRT_STAGES];
+    uint32_t attempts;       /* frame attempts: > 1 when a pool / launch bound was outgrown and the frame redone */
+    uint32_t pad;
 } jsrt_stats;
 
 typedef void (*jsrt_progress_fn)(int32_t pass, double completion, void *user);

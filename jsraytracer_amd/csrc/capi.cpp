@@ -250,6 +250,7 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
         st->kernel_ms = ms;
         st->launches = launches;
         st->batches = kt.batches;
+        st->attempts = kt.attempts;
         st->samples = (uint64_t)a.ncols * a.H * a.spp;
     }
     (void)hipFreeAsync(accum, stream);

@@ -19,6 +19,7 @@
 // budget; batches are (pixels x samples) with ray SoA buffers in HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -416,7 +417,7 @@ __device__ __forceinline__ F3 accumulate(const RenderArgs &A, F3 acc, F3 col) {
 // camera rays: one per path q of the batch, sample-major (neighbouring q are neighbouring pixels)
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-    if (!W.chain && q < 64) W.lvl[q] = q == 0 ? W.npaths : 0u;  // level counts and overflow flag
+    if (!W.chain && q < LVL_UNDER) W.lvl[q] = q == 0 ? W.npaths : 0u;  // level counts (not the frame flags)
     if (q >= W.npaths) return;
     int c = 0, py = 0, px = 0;
     const uint32_t pl = q % W.npix, sl = q / W.npix;
@@ -462,6 +463,7 @@ __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs
         if (t >= W.npaths) return;
     } else {
         const LevelRange R = level_range(W, L);
+        if (t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // the launch bound was too small
         if (t >= R.count) return;
         i = R.base + t;
     }
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         return;
     }
     if ((size_t)at + nchild > W.level_cap || (size_t)next_base + at + nchild > W.pool) {
-        W.lvl[LVL_FLAG] = 1u;  // overflow: the host redoes the batch smaller
+        W.lvl[LVL_FLAG] = 1u;  // outgrew the pool: the host redoes the frame with a larger one
         return;
     }
     const uint32_t path = W.path[r];
@@ -665,7 +667,7 @@ __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
 // tree schedule: per pixel, the batch's samples in order
 __global__ __launch_bounds__(256) void k_accum(RenderArgs A, WArgs W) {
     const uint32_t pl = blockIdx.x * 256 + threadIdx.x;
-    if (pl >= W.npix || W.lvl[LVL_FLAG]) return;  // an overflowed batch is redone by the host
+    if (pl >= W.npix || W.lvl[LVL_FLAG]) return;  // a poisoned frame is redone by the host
     int c, py, px;
     if (!pixel_of(A, W.p0 + pl, c, py, px)) return;
     const size_t oi = (size_t)c * A.H + py;
@@ -806,10 +808,12 @@ namespace {
 inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 255) / 256); }
 
 // Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.
-// Tree: each level's launch is sized by an upper bound of its ray count (the real count is on
-// the device and surplus blocks exit at once); levels are reduced bottom-up afterwards.
+// Tree: level L's launches cover bound[L] rays (the real count is on the device and surplus
+// blocks exit at once; a count above the bound sets LVL_UNDER and the frame is redone);
+// levels are reduced bottom-up afterwards.
 template <int PF, bool CHAIN>
-void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt) {
+void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
+               const std::vector<size_t> &bound) {
     auto timed = [&](int which, auto launch) {
         const bool ev = kt && kt->on(which);
         if (ev) kt->ev[which].begin(st);
@@ -817,9 +821,9 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         if (ev) kt->ev[which].end(st);
     };
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
-    std::vector<size_t> ubs;  // upper bound of each level's ray count
-    size_t ub = A.max_depth > 0 ? W.npaths : 0;
-    for (int L = 0; L < A.max_depth && ub > 0; ++L) {
+    std::vector<size_t> ubs;  // launch bound of each level's ray count
+    for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
+        const size_t ub = CHAIN ? (size_t)W.npaths : bound[L];
         ubs.push_back(ub);
         const int child_depth = A.max_depth - L - 1;
         timed(KT_EXTEND, [&] {
@@ -835,7 +839,6 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 else
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L);
             });
-        if (!CHAIN) ub = child_depth > 0 ? std::min(ub * (size_t)S.max_children, W.level_cap) : 0;
     }
     if (CHAIN) {
         timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
@@ -847,12 +850,13 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
 }
 
 template <bool CHAIN>
-void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt) {
+void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
+                  const std::vector<size_t> &bound) {
     switch (S.profile) {
-    case PF_ANALYTIC: run_batch<PF_ANALYTIC, CHAIN>(S, A, W, st, kt); break;
-    case PF_MESH: run_batch<PF_MESH, CHAIN>(S, A, W, st, kt); break;
-    case PF_SDF: run_batch<PF_SDF, CHAIN>(S, A, W, st, kt); break;
-    default: run_batch<PF_ALL, CHAIN>(S, A, W, st, kt); break;
+    case PF_ANALYTIC: run_batch<PF_ANALYTIC, CHAIN>(S, A, W, st, kt, bound); break;
+    case PF_MESH: run_batch<PF_MESH, CHAIN>(S, A, W, st, kt, bound); break;
+    case PF_SDF: run_batch<PF_SDF, CHAIN>(S, A, W, st, kt, bound); break;
+    default: run_batch<PF_ALL, CHAIN>(S, A, W, st, kt, bound); break;
     }
 }
 }  // namespace
@@ -866,82 +870,99 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     uint32_t npix = npix_total, nsb = 1;  // batch: [p0, p0 + npix) pixels x [s0, s0 + nsb) samples
     if ((size_t)npix > max_paths) npix = (uint32_t)(max_paths & ~(size_t)63);
     else nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)A.spp));
-    // Chain schedule when no node can have two children: depth x paths node records, no
-    // overflow possible, batches enqueued back to back.  Tree schedule otherwise: a ray pool for
-    // all levels of a batch (one level may hold half of it); each batch's overflow flag is read
-    // back and an overflowed batch is redone in halves (a one-patch batch grows the pool).
+    // Chain schedule when no node can have two children: depth x paths node records, nothing can
+    // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all
+    // levels of a batch (one level may hold half of it), compacted level by level.  Its launches
+    // are sized by level counts learned from the scene's first batch (one read-back per scene and
+    // batch shape) with a margin; a batch that outgrows its pool (LVL_FLAG) or a launch bound
+    // (LVL_UNDER) poisons the frame, which is redone with a larger pool / conservative bounds.
+    // The frame flags are read once, after the last batch.
     const bool chain = S.max_children <= 1;
     const int depth = std::max(1, A.max_depth);
     const size_t paths = (size_t)npix * nsb;
-    size_t pool = chain ? paths : paths * 8, level_cap = chain ? paths : pool / 2;
-    auto reserve = [&]() {
-        return chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false)
-                     : wf.reserve(pool, pool, level_cap, level_cap, true);
-    };
-    hipError_t e = reserve();
-    if (e != hipSuccess) return e;
-    WArgs W = wf.args;
-    auto setup = [&](WArgs &w) {
-        w.ns = ns;
-        w.group = 1;
+    // test knobs: a smaller first pool / tighter learned bounds exercise the frame redo paths
+    const char *pf_env = getenv("JSRT_POOL_FACTOR"), *bm_env = getenv("JSRT_BOUND_MARGIN");
+    const double margin = bm_env ? atof(bm_env) : 1.25;
+    const size_t slack = bm_env ? 0 : 4096;
+    if (!chain && wf.pool_paths != paths) {  // learned pool / bounds are per batch shape
+        wf.pool_factor = pf_env ? std::max(1, atoi(pf_env)) : 8;
+        wf.frac.clear();
+        wf.pool_paths = paths;
+    }
+    hipError_t e = hipSuccess;
+    uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree schedule)
+    if (!chain && (e = hipHostMalloc((void **)&h_lvl, 64 * sizeof(uint32_t), 0)) != hipSuccess) return e;
+    bool conservative = false;
+    for (int attempt = 0; e == hipSuccess; ++attempt) {
+        if (kt) kt->attempts = (uint32_t)attempt + 1;
+        const size_t pool = chain ? paths : paths * wf.pool_factor, level_cap = chain ? paths : pool / 2;
+        e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false)
+                  : wf.reserve(pool, pool, level_cap, level_cap, true);
+        if (e != hipSuccess) break;
+        WArgs W = wf.args;
+        W.ns = ns;
+        W.group = 1;
         if (ns > 1 && ns <= 64)
-            while (w.group < ns) w.group *= 2;
-        w.chain = chain ? 1 : 0;
-        w.pool = pool;
-        w.level_cap = level_cap;
-    };
-    setup(W);
-    if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) return e;
-    uint32_t *h_flag = nullptr;  // overflow read-back (tree schedule only)
-    if (!chain && (e = hipHostMalloc((void **)&h_flag, 16, 0)) != hipSuccess) return e;
-    const uint64_t total = (uint64_t)npix_total * A.spp;
-    uint64_t done = 0;
-    for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess; s0 += nsb) {
-        const uint32_t nb = std::min<uint32_t>(nsb, (uint32_t)A.spp - s0);
-        for (uint32_t p0 = 0; p0 < npix_total && e == hipSuccess; p0 += npix) {
-            std::vector<std::pair<uint32_t, uint32_t>> todo{{p0, std::min(npix, npix_total - p0)}};
-            while (!todo.empty() && e == hipSuccess) {
-                const auto job = todo.back();
-                todo.pop_back();
-                W.p0 = job.first;
-                W.npix = job.second;
+            while (W.group < ns) W.group *= 2;
+        W.chain = chain ? 1 : 0;
+        W.pool = pool;
+        W.level_cap = level_cap;
+        if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
+        if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
+        auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths
+            std::vector<size_t> b(depth, 0);
+            size_t ub = np;
+            for (int L = 0; L < A.max_depth && ub > 0; ++L) {
+                b[L] = ub;
+                if (!conservative && L < (int)wf.frac.size())
+                    b[L] = std::min(ub, (size_t)((double)np * wf.frac[L] * margin) + slack);
+                ub = L + 1 < A.max_depth ? std::min(ub * (size_t)S.max_children, level_cap) : 0;
+            }
+            return b;
+        };
+        const uint64_t total = (uint64_t)npix_total * A.spp;
+        uint64_t done = 0;
+        bool stop = false;
+        for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess && !stop; s0 += nsb) {
+            const uint32_t nb = std::min<uint32_t>(nsb, (uint32_t)A.spp - s0);
+            for (uint32_t p0 = 0; p0 < npix_total; p0 += npix) {
+                W.p0 = p0;
+                W.npix = std::min(npix, npix_total - p0);
                 W.s0 = s0;
-                W.npaths = job.second * nb;
-                if (chain) run_batch_pf<true>(S, A, W, st, kt);
-                else run_batch_pf<false>(S, A, W, st, kt);
+                W.npaths = W.npix * nb;
+                const std::vector<size_t> bound = chain ? std::vector<size_t>() : bounds(W.npaths);
+                if (chain) run_batch_pf<true>(S, A, W, st, kt, bound);
+                else run_batch_pf<false>(S, A, W, st, kt, bound);
                 if ((e = hipGetLastError()) != hipSuccess) break;
-                if (!chain) {  // k_accum skipped an overflowed batch; the host redoes it
-                    if ((e = hipMemcpyAsync(h_flag, W.lvl + LVL_FLAG, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) break;
-                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                    if (*h_flag) {
-                        if (job.second <= 64) {  // cannot split further: grow the pool and retry
-                            if (pool > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
-                            pool *= 2;
-                            level_cap = pool / 2;
-                            if ((e = reserve()) != hipSuccess) break;
-                            const WArgs keep = W;
-                            W = wf.args;
-                            setup(W);
-                            W.p0 = keep.p0; W.npix = keep.npix; W.s0 = keep.s0; W.npaths = keep.npaths;
-                            todo.push_back(job);
-                            continue;
-                        }
-                        const uint32_t half = ((job.second / 2) + 63) & ~63u;
-                        todo.push_back({job.first + half, job.second - half});
-                        todo.push_back({job.first, half});
-                        continue;
-                    }
-                }
-                done += (uint64_t)job.second * nb;
+                done += (uint64_t)W.npix * nb;
                 if (kt) ++kt->batches;
+                if (!chain && wf.frac.empty() && !conservative) {  // learn the level counts once
+                    if ((e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+                    if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER])
+                        for (int L = 0; L < A.max_depth; ++L) wf.frac.push_back((double)h_lvl[L] / (double)W.npaths);
+                }
+            }
+            if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
+                if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+                stop = !progress((int)(s0 + nb - 1), (double)done / (double)total);
             }
         }
-        if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
-            if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-            if (!progress((int)(s0 + nb - 1), (double)done / (double)total)) break;
+        if (e != hipSuccess || chain) break;
+        if ((e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+        if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) break;
+        if (h_lvl[LVL_FLAG]) {  // a batch outgrew the pool: twice the pool, relearn the counts
+            if (paths * wf.pool_factor > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
+            wf.pool_factor *= 2;
+            wf.frac.clear();
+        } else {  // a level outgrew its learned bound: redo with the conservative bounds
+            conservative = true;
+            wf.frac.clear();
         }
+        if (kt) kt->reset();
     }
-    if (h_flag) (void)hipHostFree(h_flag);  // its last read-back was synchronised
+    if (h_lvl) (void)hipHostFree(h_lvl);
     if (e != hipSuccess) return e;
     const bool ev = kt && kt->on(KT_FINAL);
     if (ev) kt->ev[KT_FINAL].begin(st);

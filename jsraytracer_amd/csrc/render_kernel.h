@@ -11,7 +11,8 @@
 namespace jsrt {
 
 constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of the breadth-first schedule)
-constexpr int LVL_FLAG = 63;        // overflow flag slot of WArgs::lvl (64 words)
+constexpr int LVL_FLAG = 63;        // WArgs::lvl word set when a batch outgrew its pool (frame redone)
+constexpr int LVL_UNDER = 62;       // WArgs::lvl word set when a level outgrew its launch bound
 
 struct RenderArgs {
     int32_t W, H, kind, max_depth;
@@ -65,6 +66,9 @@ struct WArgs {
 
 struct Wavefront {  // owns the batch buffers (cached per scene)
     void *mem = nullptr;
+    // tree schedule, learned per scene and batch shape: pool size (x paths) and level counts
+    size_t pool_paths = 0, pool_factor = 8;
+    std::vector<double> frac;  // level L ray count / paths of the first batch
     size_t cap_bytes = 0;
     WArgs args{};
     // rays: ray slots; nodes: node records; hands: hand-off records; paths: root colours
@@ -88,8 +92,10 @@ struct KernelTimes {
     EventPairs ev[KT_N];
     uint32_t mask = ~0u;  // stages whose launches are bracketed by events
     uint32_t batches = 0; // (pixels x samples) batches completed
+    uint32_t attempts = 0; // frame attempts (a poisoned frame is redone)
     bool on(int k) const { return (mask >> k) & 1u; }
     void reset() {
+        batches = 0;
         for (auto &p : ev) p.used = 0;
     }
 };

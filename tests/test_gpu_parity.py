@@ -79,8 +79,7 @@ def test_gpu_matches_oracle_larger(jr, case):
 
 
 def test_gpu_batching_is_invisible(jr):
-    """The wavefront schedule's batch size (paths per batch, incl. forced splitting of levels that
-    outgrow the pool) must not change a bit."""
+    """The wavefront schedule's batch size (paths per batch) must not change a bit."""
     sc = _scene(jr, "cornell_box_path")
     a, ca, s1 = sc.render(40, 40, 6, 8, 1, 11)
     b, cb, s2 = sc.render(40, 40, 6, 8, 1, 11, max_paths=640)
@@ -89,6 +88,22 @@ def test_gpu_batching_is_invisible(jr):
     c, cc, _ = _scene(jr, "bunny").render(48, 40, 2, 4, 1, 3, max_paths=64)  # Fresnel: 2 children per hit
     d, cd, _ = _scene(jr, "bunny").render(48, 40, 2, 4, 1, 3)
     assert np.array_equal(c, d) and np.array_equal(cc.view(np.uint32), cd.view(np.uint32))
+
+
+def test_gpu_frame_redo_paths(jr, monkeypatch):
+    """Tree schedule: a batch that outgrows its pool, or a level that outgrows its learned launch
+    bound, poisons the frame and the frame is redone; the result must not change a bit."""
+    blob_b, blob_c = pyoracle.golden_scene("bunny"), pyoracle.golden_scene("cornell_box_path")
+    ref_b = _scene(jr, "bunny").render(48, 40, 2, 4, 1, 3, max_paths=512)
+    ref_c = _scene(jr, "cornell_box_path").render(40, 40, 6, 8, 1, 11, max_paths=640)
+    monkeypatch.setenv("JSRT_POOL_FACTOR", "1")  # first pool far too small for Fresnel trees
+    got_b = jr.Scene(blob_b, device=0).render(48, 40, 2, 4, 1, 3, max_paths=512)
+    monkeypatch.delenv("JSRT_POOL_FACTOR")
+    monkeypatch.setenv("JSRT_BOUND_MARGIN", "0.5")  # learned bounds below the real level counts
+    got_c = jr.Scene(blob_c, device=0).render(40, 40, 6, 8, 1, 11, max_paths=640)
+    assert got_b[2]["attempts"] > 1 and got_c[2]["attempts"] == 2  # both redo paths were taken
+    for (a, ca, _), (b, cb, _) in ((ref_b, got_b), (ref_c, got_c)):
+        assert np.array_equal(a, b) and np.array_equal(ca.view(np.uint32), cb.view(np.uint32))
 
 
 def test_gpu_progress_callback(jr):
