@@ -570,17 +570,7 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, si
     const F3 P = f3(h0.x, h0.y, h0.z);
     Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
     F3 delta, L, lcol;
-#ifdef JSRT_LIGHT_UNIFORM  // one light: its record (and colour chain) through scalar loads
-    if (S.n_lights == 1) light_sample(S, S.lights[0], P, rng, delta, L, lcol);
-    else
-#endif
     light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
-#ifdef JSRT_AB_NOCAST
-    const Hit sh{DINF, -1, 0};
-#else
-    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
-#endif
-    if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) return f3(0, 0, 0);  // shadowed: contributes +0
     const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
     ShadeData sd;
     sd.N = f3(h1.x, h1.y, h1.z);
@@ -591,10 +581,21 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, si
     sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
     sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
 #ifdef JSRT_AB_NOCOLOR
-    return lcol;
+    const F3 c = lcol;
 #else
-    return light_sample_color((int)f2u(h0.w), sd, L, lcol);
+    const F3 c = light_sample_color((int)f2u(h0.w), sd, L, lcol);
 #endif
+    // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
+    // (the light behind the surface, a black material, an edge-on area light) adds the same
+    // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
+    if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return f3(0, 0, 0);
+#ifdef JSRT_AB_NOCAST
+    const Hit sh{DINF, -1, 0};
+#else
+    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
+#endif
+    if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) return f3(0, 0, 0);  // shadowed: contributes +0
+    return c;
 }
 
 template <int PF, bool CHAIN, bool SERIAL>
