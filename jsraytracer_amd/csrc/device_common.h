@@ -656,6 +656,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         atomicAdd(&g_dbg[(ANY ? 192 : 128) + 63], 1ull);
     }
 #endif
+    float flim = (float)maxD;  // (float)min(best, maxD): the cull's far limit, updated with best
     for (int i = 0; i < S.n_roots; ++i) {
         const DRoot &R = S.rootrec[i];
         const RootBound &RB = R.rb;
@@ -672,8 +673,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
             a1 = (RB.hi[2] + e - o.z) * iz;
             tn = fmaxf(tn, fminf(a0, a1));
             tf = fminf(tf, fmaxf(a0, a1));
-            const float lim = (float)(best.t < maxD ? best.t : maxD);
-            need = need && (tn <= tf) && (tf >= fminD) && (tn <= lim);
+            need = need && (tn <= tf) && (tf >= fminD) && (tn <= flim);
         }
         if (!__any(need)) continue;
 #ifdef JSRT_DBG_COUNT
@@ -685,24 +685,25 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
           }
         }
 #endif
-        if (!need) continue;
-        if (R.kind == INST_PRIM) {
+        if (!need) {  // (a divergent if, not a divergent continue: the loop itself stays uniform)
+        } else if (R.kind == INST_PRIM) {
             const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, R.prim, 0};
+                flim = (float)best.t;
                 if (ANY) live = false;
             }
-        } else if (!(PF & (PF_BVH | PF_AGG))) {
-            continue;
         } else if ((PF & PF_BVH) && R.kind == INST_BVH) {
             const double *m = R.p.inv;
             const Hit h = bvh_cast<PF, ANY>(S, S.insts[R.inst], xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
+                flim = (float)best.t;
                 if (ANY) live = false;
             }
         } else if (PF & PF_AGG) {
             nested_cast<PF, ANY>(S, R.inst, o, d, minD, maxD, transp, best);
+            flim = (float)(best.t < maxD ? best.t : maxD);
             if (ANY && best.prim >= 0) live = false;
         }
     }
