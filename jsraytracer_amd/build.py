@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libjsrt.so")
 SOURCES = ["render.hip", "capi.cpp", "scene_load.cpp"]
-HEADERS = ["device_common.h", "device_scene.h", "render_kernel.h", "scene_load.h", "sdf_program.h"]
+HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "scene_load.h", "sdf_program.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")
 

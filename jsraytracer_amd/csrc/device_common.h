@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "device_scene.h"
+#include "js_number.h"
 
 namespace jsrt {
 
@@ -52,78 +53,6 @@ __device__ __forceinline__ double js_round(double x) {  // Math.round (half towa
     return r;
 }
 __device__ __forceinline__ float or0(float x) { return (x != x || x == 0.0f) ? 0.0f : x; }  // `x || 0`
-
-// Number(v.toPrecision(8)) — ECMA-262 toPrecision (ties -> larger n) then correctly rounded parse.
-// Exact for 1e-12 <= |v| < 2^64 (128-bit products, no 128-bit division); outside that window the
-// 8-digit rounding is applied in float64 (documented in DESIGN.md; no reference scene reaches it).
-__device__ __forceinline__ double to_precision8(double v) {
-    if (!__builtin_isfinite(v)) return v;
-    if (v == 0.0) return 0.0;
-    const bool neg = v < 0;
-    const double x = fabs(v);
-    int ex;
-    const double f = frexp(x, &ex);
-    const uint64_t M = (uint64_t)ldexp(f, 53);
-    const int E = ex - 53;
-    int e10 = (int)floor(log10(x));
-    uint64_t n = 0;
-    const uint64_t P10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
-                              100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull,
-                              10000000000000ull, 100000000000000ull, 1000000000000000ull, 10000000000000000ull,
-                              100000000000000000ull, 1000000000000000000ull, 10000000000000000000ull};
-    bool ok = false;
-    for (int it = 0; it < 4; ++it) {
-        const int k = 7 - e10;
-        uint64_t q;
-        bool up;
-        if (k >= 0) {
-            if (k > 19 || E >= 0) break;
-            const unsigned __int128 num = (unsigned __int128)M * P10[k];
-            const int s = -E;
-            if (s >= 127) break;
-            const unsigned __int128 qq = num >> s;
-            const unsigned __int128 rem = num - (qq << s);
-            if (qq >= (unsigned __int128)1000000000ull) { e10 += 1; continue; }
-            q = (uint64_t)qq;
-            up = (rem << 1) >= ((unsigned __int128)1 << s);
-        } else {
-            const int m = -k;
-            if (m > 19 || ex > 64) break;
-            uint64_t num, den;
-            if (E >= 0) { num = M << E; den = P10[m]; }
-            else {
-                num = M;
-                if (-E > 63 || P10[m] > (~0ull >> -E)) break;
-                den = P10[m] << -E;
-            }
-            q = num / den;
-            const uint64_t rem = num - q * den;
-            up = rem >= den - rem;  // 2*rem >= den without overflow
-        }
-        if (q < 10000000ull) { e10 -= 1; continue; }
-        if (q >= 100000000ull) { e10 += 1; continue; }
-        n = q + (up ? 1 : 0);
-        if (n == 100000000ull) { n = 10000000ull; e10 += 1; }
-        ok = true;
-        break;
-    }
-    double r;
-    if (!ok) {  // outside the exact window
-        const double sc = pow(10.0, (double)(7 - e10));
-        r = floor(x * sc + 0.5) / sc;
-    } else {
-        const int k2 = e10 - 7;
-        const double P10D[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-        if (k2 >= 0 && k2 <= 22) r = (double)n * P10D[k2];
-        else if (k2 < 0 && -k2 <= 22) r = (double)n / P10D[-k2];
-        else r = (double)n * pow(10.0, (double)k2);
-    }
-    return neg ? -r : r;
-}
-__device__ __forceinline__ double js_fmod(double a, double b) {  // math.js:27
-    return to_precision8(a - (floor(a / b) * b));
-}
 
 // --------------------------------------------------------------------------------------------
 // keyed RNG (oracle/refharness/keyed_rng.js)
@@ -247,80 +176,114 @@ __device__ __forceinline__ double tri_intersect(const DTri &T, F3 o, F3 d) {  //
 
 // --------------------------------------------------------------------------------------------
 // SDF program VM (sdf_program.h).  P is the 4-vector point with w == 1.
+//
+// Every lane that runs the VM runs the same program in lockstep (the wave marches one SDF), so the
+// program counter, the stack pointers and the loop counters are wave-uniform: they are kept in
+// SGPRs (readfirstlane), instruction fetch is a scalar load and the opcode switch is a scalar
+// branch.  The stacks are small fixed register files indexed by those uniform values.
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <int N>
+struct RegFile {  // per-lane doubles addressed by a wave-uniform index
+    double r[N];
+    __device__ __forceinline__ double get(int i) const {
+        double v = r[0];
+#pragma unroll
+        for (int k = 1; k < N; ++k)
+            if (i == k) v = r[k];
+        return v;
+    }
+    __device__ __forceinline__ void set(int i, double v) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (i == k) r[k] = v;
+    }
+};
+
 __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P) {
-    double dst[SDF_MAX_D];
-    F3 pst[SDF_MAX_P];
-    double sst[SDF_MAX_S];
-    int lc[SDF_MAX_LOOP];
+    RegFile<SDF_MAX_D> dst;
+    RegFile<SDF_MAX_S> sst;
+    F3 pst0 = P, pst1 = P;  // SDF_MAX_P == 2
+    int lc0 = 0, lc1 = 0;   // SDF_MAX_LOOP == 2
     int dsp = 0, psp = 0, ssp = 0, lsp = 0;
     const SdfInsn *code = S.sdf_insn;
     const double *K = S.sdf_const;
+    pc = uni(pc);  // uniform among the active lanes (sdf_node_dist's waterfall)
+    end = uni(end);
     while (pc < end) {
         const SdfInsn I = code[pc];
-        switch (I.op) {
+        const int op = uni(I.op), ia = uni(I.a), ib = uni(I.b);
+        switch (op) {
         case SOP_END: pc = end; continue;
         case SOP_BOX: {  // BoxSDF.distanceComp (sdf.js:276-279)
             // q = p.abs().minus(size).to4(0); Vec.max(q, 0).norm() + min(max(q0,q1,q2), 0)
-            const float qx = fabsf(P.x) - (float)K[I.a];
-            const float qy = or0(fabsf(P.y) - (float)K[I.a + 1]);
-            const float qz = or0(fabsf(P.z) - (float)K[I.a + 2]);
+            const float qx = fabsf(P.x) - (float)K[ia];
+            const float qy = or0(fabsf(P.y) - (float)K[ia + 1]);
+            const float qz = or0(fabsf(P.z) - (float)K[ia + 2]);
             const F3 m = f3((float)js_max(qx, 0), (float)js_max(qy, 0), (float)js_max(qz, 0));
-            dst[dsp++] = sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0);
+            dst.set(dsp++, sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0));
             break;
         }
         case SOP_SPHERE: {  // p.to4(0).norm() - radius (sdf.js:232-234)
             const F3 q = f3(P.x, or0(P.y), or0(P.z));
-            dst[dsp++] = sqrt(dot3(q, q)) - K[I.a];
+            dst.set(dsp++, sqrt(dot3(q, q)) - K[ia]);
             break;
         }
         case SOP_TETRA:  // sdf.js:305-308
-            dst[dsp++] = (js_max(fabs((double)P.x + (double)P.y) - (double)P.z,
-                                 fabs((double)P.x - (double)P.y) + (double)P.z) - 1) / sqrt(3.0);
+            dst.set(dsp++, (js_max(fabs((double)P.x + (double)P.y) - (double)P.z,
+                                   fabs((double)P.x - (double)P.y) + (double)P.z) - 1) / sqrt(3.0));
             break;
         case SOP_MIN: {
-            double r = dst[dsp - I.a];
-            for (int i = 1; i < I.a; ++i) r = js_min(r, dst[dsp - I.a + i]);
-            dsp -= I.a;
-            dst[dsp++] = r;
+            double r = dst.get(dsp - ia);
+            for (int i = 1; i < ia; ++i) r = js_min(r, dst.get(dsp - ia + i));
+            dsp -= ia;
+            dst.set(dsp++, r);
             break;
         }
         case SOP_MAX: {
-            double r = dst[dsp - I.a];
-            for (int i = 1; i < I.a; ++i) r = js_max(r, dst[dsp - I.a + i]);
-            dsp -= I.a;
-            dst[dsp++] = r;
+            double r = dst.get(dsp - ia);
+            for (int i = 1; i < ia; ++i) r = js_max(r, dst.get(dsp - ia + i));
+            dsp -= ia;
+            dst.set(dsp++, r);
             break;
         }
-        case SOP_NEG: dst[dsp - 1] = -dst[dsp - 1]; break;
-        case SOP_SUBK: dst[dsp - 1] = dst[dsp - 1] - K[I.a]; break;
+        case SOP_NEG: dst.set(dsp - 1, -dst.get(dsp - 1)); break;
+        case SOP_SUBK: dst.set(dsp - 1, dst.get(dsp - 1) - K[ia]); break;
         case SOP_SMIN: {  // smoothMin (sdf.js:128-131)
-            const double b = dst[--dsp], a = dst[dsp - 1], k = K[I.a];
+            const double b = dst.get(--dsp), a = dst.get(dsp - 1), k = K[ia];
             const double h = js_max(k - fabs(a - b), 0.0) / k;
-            dst[dsp - 1] = js_min(a, b) - h * h * h * k * (1.0 / 6.0);
+            dst.set(dsp - 1, js_min(a, b) - h * h * h * k * (1.0 / 6.0));
             break;
         }
-        case SOP_PUSHP: pst[psp++] = P; break;
-        case SOP_POPP: P = pst[--psp]; break;
-        case SOP_TPUSH: sst[ssp++] = 1.0; break;
+        case SOP_PUSHP:
+            if (psp == 0) pst0 = P;
+            else pst1 = P;
+            ++psp;
+            break;
+        case SOP_POPP:
+            --psp;
+            P = psp == 0 ? pst0 : pst1;
+            break;
+        case SOP_TPUSH: sst.set(ssp++, 1.0); break;
         case SOP_TPOP: --ssp; break;
         case SOP_TPOP_MUL: {
-            const double st = sst[--ssp];
-            sst[ssp - 1] = sst[ssp - 1] * st;
+            const double st = sst.get(--ssp);
+            sst.set(ssp - 1, sst.get(ssp - 1) * st);
             break;
         }
-        case SOP_MULS: dst[dsp - 1] = dst[dsp - 1] * sst[ssp - 1]; break;
+        case SOP_MULS: dst.set(dsp - 1, dst.get(dsp - 1) * sst.get(ssp - 1)); break;
         case SOP_XMAT:  // SDFMatrixTransformer.transform (sdf.js:433-435)
-            P = xf_point(K + I.a, P);
-            sst[ssp - 1] = sst[ssp - 1] * K[I.b];
+            P = xf_point(K + ia, P);
+            sst.set(ssp - 1, sst.get(ssp - 1) * K[ib]);
             break;
         case SOP_XREF: {  // SDFReflectionTransformer.transformComp (sdf.js:450-455)
-            const F3 n = f3((float)K[I.a], (float)K[I.a + 1], (float)K[I.a + 2]);
-            const double dt = dot3(n, P) - K[I.a + 3];
+            const F3 n = f3((float)K[ia], (float)K[ia + 1], (float)K[ia + 2]);
+            const double dt = dot3(n, P) - K[ia + 3];
             if (dt < 0) P = sub(P, scale(n, 2 * dt));
             break;
         }
         case SOP_XREP: {  // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473)
-            const double sx = K[I.a], sy = K[I.a + 1], sz = K[I.a + 2];
+            const double sx = K[ia], sy = K[ia + 1], sz = K[ia + 2];
             const float x = (float)(js_fmod((double)P.x + sx / 2, sx) - sx / 2);
             const float y = (float)(js_fmod((double)P.y + sy / 2, sy) - sy / 2);
             const float z = (float)(js_fmod((double)P.z + sz / 2, sz) - sz / 2);
@@ -328,22 +291,40 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
             break;
         }
         case SOP_LOOP:
-            if (I.a <= 0) { pc = I.b + 1; continue; }
-            lc[lsp++] = I.a;
+            if (ia <= 0) { pc = ib + 1; continue; }
+            if (lsp == 0) lc0 = ia;
+            else lc1 = ia;
+            ++lsp;
             break;
-        case SOP_ENDLOOP:
-            if (--lc[lsp - 1] > 0) { pc = I.a + 1; continue; }
+        case SOP_ENDLOOP: {
+            int c = (lsp == 1 ? lc0 : lc1) - 1;
+            if (lsp == 1) lc0 = c;
+            else lc1 = c;
+            if (c > 0) { pc = ia + 1; continue; }
             --lsp;
             break;
+        }
         default: break;
         }
         ++pc;
     }
-    return dst[0];
+    return dst.get(0);
 }
 
+// Lanes may ask for different nodes (getMaterialData picks children per lane, a BVH leaf may hold
+// different SDF primitives): a waterfall runs the VM once per distinct program among the active
+// lanes, each time with a uniform program counter.
 __device__ __forceinline__ double sdf_node_dist(const DScene &S, int n, F3 p) {
-    return sdf_run(S, S.sdf_range[2 * n], S.sdf_range[2 * n + 1], p);
+    const int pc = S.sdf_range[2 * n], end = S.sdf_range[2 * n + 1];
+    double r = 0;
+    for (;;) {
+        const int pcu = uni(pc);
+        if (pc == pcu) {
+            r = sdf_run(S, pcu, end, p);
+            break;
+        }
+    }
+    return r;
 }
 
 __device__ __forceinline__ double sdf_intersect(const DScene &S, int g, F3 o, F3 d, double minD, double maxD) {  // sdf.js:12-40
@@ -708,6 +689,153 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         }
     }
     return best;
+}
+
+// --------------------------------------------------------------------------------------------
+// Persistent casts for SDF scenes (world.js:7-15 + sdf.js:12-40 with lane refill).
+//
+// A sphere-traced SDF takes anywhere from a few to max_samples steps per ray, so a wave that casts
+// 64 rays together idles most lanes while its slowest ray marches (measured: 15 % VALU lane use on
+// SDF_Menger).  Here each lane runs a resumable World.cast: it walks the top-level objects in
+// World.objects order (culling and exact tests exactly as world_cast), suspends at an SDF
+// primitive to march it, and every iteration of the kernel's loop performs ONE march step for all
+// marching lanes together (one uniform SDF program, sdf_node_dist).  A lane whose cast finishes
+// stores its hit and takes the next ray from a work counter (one atomic per wave and round).
+// Objects are still visited in order with the same acceptance tests, so the closest hit (first
+// minimum) is unchanged bit for bit.  Top level must be primitives only (all_roots_prims).
+struct MarchState {
+    F3 o, d;          // world ray
+    F3 lo, ld;        // ray in the SDF primitive's frame
+    double t, tmin, tmax, rdn;
+    Hit best;
+    float flim;
+    int root;         // next top-level object to visit
+    int steps, g, prim;
+    bool marching;
+};
+
+// The conservative world-box cull of world_cast for one top-level object.
+__device__ __forceinline__ bool root_needed(const RootBound &RB, F3 o, float ix, float iy, float iz, float oabs,
+                                            float fminD, float flim) {
+    if (!RB.bounded) return true;
+    const float e = RB.k * oabs + RB.e0;
+    float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
+    float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
+    a0 = (RB.lo[1] - e - o.y) * iy;
+    a1 = (RB.hi[1] + e - o.y) * iy;
+    tn = fmaxf(tn, fminf(a0, a1));
+    tf = fminf(tf, fmaxf(a0, a1));
+    a0 = (RB.lo[2] - e - o.z) * iz;
+    a1 = (RB.hi[2] + e - o.z) * iz;
+    tn = fmaxf(tn, fminf(a0, a1));
+    tf = fminf(tf, fmaxf(a0, a1));
+    return (tn <= tf) && (tf >= fminD) && (tn <= flim);
+}
+
+// Advance a lane's cast through the top-level objects until it must march an SDF primitive
+// (returns with m.marching) or the cast is complete (m.root == n_roots).
+template <int PF, bool ANY>
+__device__ __forceinline__ void march_advance(const DScene &S, MarchState &m, double minD, double maxD, bool transp) {
+    const float ix = __builtin_amdgcn_rcpf(m.d.x), iy = __builtin_amdgcn_rcpf(m.d.y), iz = __builtin_amdgcn_rcpf(m.d.z);
+    const float oabs = fmaxf(fabsf(m.o.x), fmaxf(fabsf(m.o.y), fabsf(m.o.z)));
+    const float fminD = (float)minD;
+    while (m.root < S.n_roots) {
+        const DRoot &R = S.rootrec[m.root++];
+        if (!root_needed(R.rb, m.o, ix, iy, iz, oabs, fminD, m.flim)) continue;
+        const DPrim &P = R.p;
+        if ((PF & PF_SDF) && P.gkind == JSRT_GEOM_SDF) {  // Primitive.intersect -> SDFGeometry.intersect
+            if (!transp && !P.casts_shadow) continue;   // Infinity: never accepted
+            const F3 lo = xf_point(P.inv, m.o), ld = xf_dir(P.inv, m.d);
+            const jsrt_rec_sdfgeom &G = S.sdfg[P.gindex];
+            double bmin, bmax;
+            if (!aabb_slab(G.center[0], G.center[1], G.center[2], G.half[0], G.half[1], G.half[2], lo, ld, minD, maxD,
+                           bmin, bmax))
+                continue;
+            if (G.max_samples <= 0) continue;
+            m.lo = lo;
+            m.ld = ld;
+            m.tmin = js_max(minD, bmin);
+            m.tmax = js_min(maxD, bmax);
+            m.t = m.tmin;
+            m.rdn = sqrt(dot3(ld, ld));
+            m.steps = 0;
+            m.g = P.gindex;
+            m.prim = R.prim;
+            m.marching = true;
+            return;
+        }
+        const double t = prim_intersect<PF>(S, P, m.o, m.d, minD, maxD, transp, fmin(maxD, m.best.t));
+        if (t > minD && t < m.best.t && t < maxD) {
+            m.best = Hit{t, R.prim, 0};
+            m.flim = (float)m.best.t;
+            if (ANY) m.root = S.n_roots;
+        }
+    }
+}
+
+// One sphere-tracing step of a marching lane (the body of sdf_intersect's loop).
+template <bool ANY>
+__device__ __forceinline__ void march_step(const DScene &S, MarchState &m, double minD, double maxD) {
+    const jsrt_rec_sdfgeom &G = S.sdfg[m.g];
+    const double distance = sdf_node_dist(S, G.root, ray_point(m.lo, m.ld, m.t));
+    bool end = false, hit = false;
+    if (!__builtin_isfinite(distance)) end = true;
+    else if (distance <= G.eps) end = hit = true;
+    else {
+        m.t += distance / m.rdn;
+        if (m.t < m.tmin || m.t > m.tmax || (m.t - m.tmin) * m.rdn > G.max_trace || ++m.steps >= G.max_samples)
+            end = true;
+    }
+    if (!end) return;
+    m.marching = false;
+    if (hit && m.t > minD && m.t < m.best.t && m.t < maxD) {
+        m.best = Hit{m.t, m.prim, 0};
+        m.flim = (float)m.best.t;
+        if (ANY) m.root = S.n_roots;
+    }
+}
+
+// The persistent loop.  Src: bool load(uint32_t job, F3 &o, F3 &d) (false: no ray in that slot),
+// void store(uint32_t job, const Hit &h).  Jobs [0, count) are taken from *ctr.
+template <int PF, bool ANY, class Src>
+__device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, uint32_t count, double minD,
+                                                double maxD, bool transp, Src &src) {
+    MarchState m;
+    m.marching = false;
+    bool have = false, drained = false;
+    uint32_t job = 0;
+    const int lane = (int)__lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (;;) {
+        const bool want = !have && !drained;
+        const uint64_t wb = __ballot(want);
+        if (wb) {
+            const int leader = __builtin_ctzll(wb);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(wb));
+            base = __shfl(base, leader);
+            if (want) {
+                job = base + (uint32_t)__popcll(wb & lt);
+                if (job >= count) drained = true;
+                else if (src.load(job, m.o, m.d)) {
+                    have = true;
+                    m.best = Hit{DINF, -1, 0};
+                    m.flim = (float)maxD;
+                    m.root = 0;
+                    m.marching = false;
+                }
+            }
+        }
+        if (!__any(have || !drained)) break;
+        if (have && !m.marching) {
+            march_advance<PF, ANY>(S, m, minD, maxD, transp);
+            if (!m.marching) {
+                src.store(job, m.best);
+                have = false;
+            }
+        }
+        if (have && m.marching) march_step<ANY>(S, m, minD, maxD);
+    }
 }
 
 // --------------------------------------------------------------------------------------------

@@ -1,0 +1,145 @@
+// js_number.h — the reference's Math.fmod rounding (math.js:27: Number(x.toPrecision(8))), on the
+// host and the device.  SDFInfiniteRepetitionTransformer (sdf.js:471-473) and the checkerboard
+// colour (materials.js:72-75) call it per evaluation, so it sits on the SDF march's inner loop.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace jsrt {
+
+// Number(v.toPrecision(8)) — ECMA-262 toPrecision (ties -> larger n) then correctly rounded parse.
+// Exact for 1e-12 <= |v| < 2^64 (128-bit products, no 128-bit division); outside that window the
+// 8-digit rounding is applied in float64 (documented in DESIGN.md; no reference scene reaches it).
+__host__ __device__ inline double to_precision8_exact(double v) {
+    if (!__builtin_isfinite(v)) return v;
+    if (v == 0.0) return 0.0;
+    const bool neg = v < 0;
+    const double x = fabs(v);
+    int ex;
+    const double f = frexp(x, &ex);
+    const uint64_t M = (uint64_t)ldexp(f, 53);
+    const int E = ex - 53;
+    int e10 = (int)floor(log10(x));
+    uint64_t n = 0;
+    const uint64_t P10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                              100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull,
+                              10000000000000ull, 100000000000000ull, 1000000000000000ull, 10000000000000000ull,
+                              100000000000000000ull, 1000000000000000000ull, 10000000000000000000ull};
+    bool ok = false;
+    for (int it = 0; it < 4; ++it) {
+        const int k = 7 - e10;
+        uint64_t q;
+        bool up;
+        if (k >= 0) {
+            if (k > 19 || E >= 0) break;
+            const unsigned __int128 num = (unsigned __int128)M * P10[k];
+            const int s = -E;
+            if (s >= 127) break;
+            const unsigned __int128 qq = num >> s;
+            const unsigned __int128 rem = num - (qq << s);
+            if (qq >= (unsigned __int128)1000000000ull) { e10 += 1; continue; }
+            q = (uint64_t)qq;
+            up = (rem << 1) >= ((unsigned __int128)1 << s);
+        } else {
+            const int m = -k;
+            if (m > 19 || ex > 64) break;
+            uint64_t num, den;
+            if (E >= 0) { num = M << E; den = P10[m]; }
+            else {
+                num = M;
+                if (-E > 63 || P10[m] > (~0ull >> -E)) break;
+                den = P10[m] << -E;
+            }
+            q = num / den;
+            const uint64_t rem = num - q * den;
+            up = rem >= den - rem;  // 2*rem >= den without overflow
+        }
+        if (q < 10000000ull) { e10 -= 1; continue; }
+        if (q >= 100000000ull) { e10 += 1; continue; }
+        n = q + (up ? 1 : 0);
+        if (n == 100000000ull) { n = 10000000ull; e10 += 1; }
+        ok = true;
+        break;
+    }
+    double r;
+    if (!ok) {  // outside the exact window
+        // 10^(7-e10) in two factors: a single one overflows for denormal x (5e-324 -> 10^331)
+        const int k = 7 - e10, k1 = k / 2;
+        const double s1 = pow(10.0, (double)k1), s2 = pow(10.0, (double)(k - k1));
+        r = floor(x * s1 * s2 + 0.5) / s2 / s1;
+    } else {
+        const int k2 = e10 - 7;
+        const double P10D[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        if (k2 >= 0 && k2 <= 22) r = (double)n * P10D[k2];
+        else if (k2 < 0 && -k2 <= 22) r = (double)n / P10D[-k2];
+        else r = (double)n * pow(10.0, (double)k2);
+    }
+    return neg ? -r : r;
+}
+
+// Fast path for 1e-37 <= |v| < 1e8 (every value the reference scenes produce).  The product
+// x * 10^k is carried as p + err: for k <= 22 one fma gives the exact rounding error; for k in
+// 23..44 it is x * 1e22 * 10^(k-22) in double-double (err then carries ~2^-100 relative error,
+// which decides a rounding only for a product within that distance of a half-integer; an exact
+// tie needs x * 10^k to be a multiple of 1/2, impossible for x < 1e-15).  The 8-digit integer n
+// (ties -> larger n, ECMA-262 toPrecision) follows without 128-bit arithmetic:
+//   * p and r = floor(p) are multiples of ulp(p) <= 2^-26 and p - r is exact, so err only
+//     matters when p - r == 0.5 (err > 0 rounds up, err < 0 down, 0 is a tie, rounded up);
+//   * the decade test x * 10^k < 1e7 is p < 1e7, or p == 1e7 with err < 0 (likewise for 1e8).
+// The parse n * 10^(e10-7) is one correctly rounded IEEE multiply or divide by an exact power of
+// ten for |e10 - 7| <= 22, else a division by 1e22 * 10^j with a remainder correction.  The
+// k <= 22 range is bit-identical to to_precision8_exact (tests/test_js_number.py).
+__host__ __device__ inline double to_precision8(double v) {
+    if (!__builtin_isfinite(v)) return v;
+    if (v == 0.0) return 0.0;
+    const double x = fabs(v);
+    int ex;
+    (void)frexp(x, &ex);  // x in [2^(ex-1), 2^ex)
+    int e10 = (int)floor((double)(ex - 1) * 0.30102999566398120);  // floor(log10 x) or one less
+    const double P10D[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                             1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    for (int it = 0; it < 3; ++it) {
+        const int k = 7 - e10;
+        if (k > 44 && it == 0) { e10 += 1; continue; }  // the estimate may be one decade low
+        if (k < 0 || k > 44) break;
+        double p, err;
+        if (k <= 22) {
+            const double P = P10D[k];
+            p = x * P;
+            err = fma(x, P, -p);
+        } else {
+            const double B = P10D[k - 22];
+            const double p1 = x * 1e22, e1 = fma(x, 1e22, -p1);
+            p = p1 * B;
+            err = fma(p1, B, -p) + e1 * B;
+        }
+        if (p < 1e7 || (p == 1e7 && err < 0)) { e10 -= 1; continue; }
+        if (p > 1e8 || (p == 1e8 && err >= 0)) { e10 += 1; continue; }
+        const double r = floor(p), fr = p - r;
+        double n = r + ((fr > 0.5 || (fr == 0.5 && err >= 0)) ? 1.0 : 0.0);
+        int e = e10;
+        if (n == 1e8) { n = 1e7; e += 1; }
+        const int k2 = e - 7;
+        double res;
+        if (k2 >= 0) {
+            res = n * P10D[k2];  // k2 <= 0 here: e10 <= 7
+        } else if (-k2 <= 22) {
+            res = n / P10D[-k2];
+        } else {  // n / (1e22 * B): quotient and exact remainders, one final rounding
+            const double B = P10D[-k2 - 22];
+            const double q1 = n / 1e22, r1 = fma(-q1, 1e22, n);
+            const double q = q1 / B, r = fma(-q, B, q1);
+            res = q + (r + r1 / 1e22) / B;
+        }
+        return v < 0 ? -res : res;
+    }
+    return to_precision8_exact(v);
+}
+
+__host__ __device__ inline double js_fmod(double a, double b) {  // math.js:27
+    return to_precision8(a - (floor(a / b) * b));
+}
+
+}  // namespace jsrt

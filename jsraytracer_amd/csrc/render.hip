@@ -564,12 +564,15 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
 // W.group lanes serve one node (sample s on lane s, a power of two >= ns); the node's first lane
 // adds the samples in the reference's order from its neighbours' registers.  SERIAL (more than 64
 // samples per node, group 1): one lane per node walks all samples itself.
+// One light sample of a lit node without its shadow cast: the light sample (lights.js), its
+// unshadowed colour (colorFromLightSample) and the shadow ray (origin P = the hit point, direction
+// delta, accepted distances (1e-4, 1), materials.js:250-252).
 template <int PF>
-__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s) {
+__device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
     const float4 h0 = hp[0];
-    const F3 P = f3(h0.x, h0.y, h0.z);
+    P = f3(h0.x, h0.y, h0.z);
     Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
-    F3 delta, L, lcol;
+    F3 L, lcol;
     light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
     const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
     ShadeData sd;
@@ -581,10 +584,18 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, si
     sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
     sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
 #ifdef JSRT_AB_NOCOLOR
-    const F3 c = lcol;
+    return lcol;
 #else
-    const F3 c = light_sample_color((int)f2u(h0.w), sd, L, lcol);
+    return light_sample_color((int)f2u(h0.w), sd, L, lcol);
 #endif
+}
+
+__device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
+
+template <int PF>
+__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s) {
+    F3 P, delta;
+    const F3 c = sample_unshadowed<PF>(S, hp, hs, s, P, delta);
     // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
@@ -594,8 +605,27 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, si
 #else
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
 #endif
-    if (sh.prim >= 0 && sh.t > 0 && sh.t < 1) return f3(0, 0, 0);  // shadowed: contributes +0
+    if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
     return c;
+}
+
+// colorFromLights: per light, its samples in order (a shadowed sample adds +0, which never changes
+// an f32 running sum that starts at +0), times 1/samples, added to the ambient `ret`.  Sample s of
+// the node sits on lane (lane & ~(G - 1)) + s; every lane takes part in the shuffles.
+__device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3 c) {
+    const int lane0 = (int)(__lane_id() & ~(G - 1));
+    uint32_t k = 0;
+    for (int li = 0; li < S.n_lights; ++li) {
+        const DLight &Lt = S.lights[li];
+        const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
+        F3 light_color = f3(0, 0, 0);
+        for (int j = 0; j < n; ++j, ++k) {
+            const int src = lane0 + (int)k;
+            light_color = add(light_color, f3(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src)));
+        }
+        if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
+    }
+    return ret;
 }
 
 template <int PF, bool CHAIN, bool SERIAL>
@@ -630,20 +660,114 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     }
     F3 c = f3(0, 0, 0);
     if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s);
-    // colorFromLights: per light, its samples in order (a shadowed sample adds +0, which never
-    // changes an f32 running sum that starts at +0), times 1/samples; every lane takes part
-    const int lane0 = (int)(__lane_id() & ~(G - 1));
-    uint32_t k = 0;
-    for (int li = 0; li < S.n_lights; ++li) {
-        const DLight &Lt = S.lights[li];
-        const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
-        F3 light_color = f3(0, 0, 0);
-        for (int j = 0; j < n; ++j, ++k) {
-            const int src = lane0 + (int)k;
-            light_color = add(light_color, f3(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src)));
-        }
-        if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
+    ret = light_sums(S, G, ret, c);
+    if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent casts for SDF scenes (device_common.h persistent_cast): same results as k_extend /
+// k_shadow, with lanes refilled from a work counter while other lanes keep marching.
+struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
+    const WArgs &W;
+    uint32_t base;
+    __device__ __forceinline__ bool load(uint32_t j, F3 &o, F3 &d) const {
+        const uint32_t i = base + j;
+        if (W.prim[i] == NO_RAY) return false;
+        o = f3(W.ox[i], W.oy[i], W.oz[i]);
+        d = f3(W.dx[i], W.dy[i], W.dz[i]);
+        return true;
     }
+    __device__ __forceinline__ void store(uint32_t j, const Hit &h) const {
+        const uint32_t i = base + j;
+        W.t[i] = h.t;
+        W.prim[i] = h.prim;
+        W.ctx[i] = h.ctx;
+    }
+};
+
+template <int PF, bool CHAIN>
+__global__ __launch_bounds__(256) void k_extend_q(DScene S, WArgs W, int L, double minD) {
+    uint32_t count = W.npaths, base = 0;
+    if (!CHAIN) {
+        const LevelRange R = level_range(W, L);
+        count = R.count;
+        base = R.base;
+    }
+    ExtendSrc src{W, base};
+    persistent_cast<PF, false>(S, W.qctr + L, count, minD, DINF, true, src);
+}
+
+struct ShadowSrc {  // the light samples' shadow rays written by k_shadow_prep
+    const WArgs &W;
+    __device__ __forceinline__ bool load(uint32_t e, F3 &o, F3 &d) const {
+        const float4 c = W.scol[e];
+        if (f2u(c.w) != 1u) return false;
+        const float4 a = W.sray[e], b = W.sray[W.sstride + e];
+        o = f3(a.x, a.y, a.z);
+        d = f3(b.x, b.y, b.z);
+        return true;
+    }
+    __device__ __forceinline__ void store(uint32_t e, const Hit &h) const {
+        if (shadowed(h)) W.scol[e].w = u2f(2u);
+    }
+};
+
+// k_shadow's lane layout (node q on lanes [q * G, q * G + G), sample s on lane s): the unshadowed
+// colour and shadow ray of every light sample
+template <int PF, bool CHAIN>
+__global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
+    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
+    if (!CHAIN) {
+        const LevelRange R = level_range(W, L);
+        count = R.count;
+        base = R.base;
+    }
+    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t q = e / G, s = e % G;
+    if (q >= count || s >= ns) return;
+    const float4 nd = W.node[base + q];
+    if (!(f2u(nd.w) & INFO_LIT)) return;
+    F3 P, delta;
+    const F3 c = sample_unshadowed<PF>(S, W.hand + q, W.hstride, s, P, delta);
+    const bool cast = !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f);  // see sample_color
+    W.scol[e] = make_float4(c.x, c.y, c.z, u2f(cast ? 1u : 0u));
+    if (cast) {
+        W.sray[e] = make_float4(P.x, P.y, P.z, 0.0f);
+        W.sray[W.sstride + e] = make_float4(delta.x, delta.y, delta.z, 0.0f);
+    }
+}
+
+template <int PF, bool CHAIN>
+__global__ __launch_bounds__(256) void k_shadow_cast(DScene S, WArgs W, int L) {
+    uint32_t count = W.npaths;
+    if (!CHAIN) count = level_range(W, L).count;
+    ShadowSrc src{W};
+    persistent_cast<PF, true>(S, W.qctr + 32 + L, count * (uint32_t)W.group, 0.0001, 1, false, src);
+}
+
+// colorFromLights' sums of k_shadow from the stored sample colours (shadowed: +0)
+template <bool CHAIN>
+__global__ __launch_bounds__(256) void k_shadow_sum(DScene S, WArgs W, int L) {
+    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
+    if (!CHAIN) {
+        const LevelRange R = level_range(W, L);
+        count = R.count;
+        base = R.base;
+    }
+    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t q = e / G, s = e % G;
+    const bool in = q < count;
+    const uint32_t i = base + (in ? q : 0u);
+    const float4 nd = W.node[i];
+    const bool lit = in && (f2u(nd.w) & INFO_LIT);
+    F3 c = f3(0, 0, 0);
+    if (lit && s < ns) {
+        const float4 v = W.scol[e];
+        if (f2u(v.w) != 2u) c = f3(v.x, v.y, v.z);
+    }
+    const F3 ret = light_sums(S, G, f3(nd.x, nd.y, nd.z), c);
     if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
 
@@ -767,13 +891,14 @@ EventPairs::~EventPairs() {
     for (auto x : e) (void)hipEventDestroy(x);
 }
 
-hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree) {
+hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree, size_t shadow) {
     size_t bytes = 0;
     bytes += 8 * need(rays, 4) + need(rays, 8) + 2 * need(rays, 4);  // o d addr key + t + prim ctx
     if (tree) bytes += 2 * need(rays, 4);                            // path parent
     bytes += need(nodes, 16) + need(4 * nodes, 16);                  // node + child
     if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
     bytes += need(7 * hands, 16) + need(64, 4);                      // hand-off + level counts
+    bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
     } else {
         if (mem) (void)hipFree(mem);
@@ -796,8 +921,11 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree) { w.slot = carve<float4>(p, 2 * nodes); w.root = carve<float>(p, 3 * paths); }
     w.hand = carve<float4>(p, 7 * hands);
     w.lvl = carve<uint32_t>(p, 64);
+    w.qctr = carve<uint32_t>(p, 64);
+    if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
     w.nstride = nodes;
     w.hstride = hands;
+    w.sstride = shadow;
     return hipSuccess;
 }
 
@@ -807,6 +935,25 @@ Wavefront::~Wavefront() {
 
 namespace {
 inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 255) / 256); }
+
+// Grid of a persistent kernel: as many 256-thread blocks as the device keeps resident (occupancy x
+// CUs), never more than the work needs.  Cached per kernel and device.
+unsigned persistent_grid(const void *kernel, size_t work) {
+    static std::vector<std::pair<std::pair<const void *, int>, unsigned>> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    unsigned resident = 0;
+    for (auto &c : cache)
+        if (c.first.first == kernel && c.first.second == dev) resident = c.second;
+    if (!resident) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+        resident = (unsigned)(per_cu * cus);
+        cache.push_back({{kernel, dev}, resident});
+    }
+    return std::max(1u, std::min(resident, grid_ub(work)));
+}
 
 // Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.
 // Tree: level L's launches cover bound[L] rays (the real count is on the device and surplus
@@ -821,6 +968,9 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         launch();
         if (ev) kt->ev[which].end(st);
     };
+    // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
+    const bool Q = (PF & PF_SDF) && W.sstride != 0;
+    if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
     std::vector<size_t> ubs;  // launch bound of each level's ray count
     for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
@@ -828,14 +978,24 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         ubs.push_back(ub);
         const int child_depth = A.max_depth - L - 1;
         timed(KT_EXTEND, [&] {
-            hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
+            if (Q)
+                hipLaunchKernelGGL((k_extend_q<PF, CHAIN>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN>, ub)),
+                                   dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
+            else
+                hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
         });
         if (W.ns > 0)
             timed(KT_SHADOW, [&] {
-                if (W.ns <= 64)
+                const size_t ne = ub * (size_t)W.group;
+                if (Q && W.ns <= 64) {
+                    hipLaunchKernelGGL((k_shadow_prep<PF, CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
+                    hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN>), dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN>, ne)),
+                                       dim3(256), 0, st, S, W, L);
+                    hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
+                } else if (W.ns <= 64)
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), 0, st, S, W, L);
                 else
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L);
@@ -897,14 +1057,20 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     for (int attempt = 0; e == hipSuccess; ++attempt) {
         if (kt) kt->attempts = (uint32_t)attempt + 1;
         const size_t pool = chain ? paths : paths * wf.pool_factor, level_cap = chain ? paths : pool / 2;
-        e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false)
-                  : wf.reserve(pool, pool, level_cap, level_cap, true);
+        int group = 1;
+        if (ns > 1 && ns <= 64)
+            while (group < ns) group *= 2;
+        // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
+        const char *pe = getenv("JSRT_PERSIST");
+        const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
+        const size_t hands = chain ? paths : level_cap;
+        const size_t shadow = persist ? hands * (size_t)group : 0;
+        e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
+                  : wf.reserve(pool, pool, level_cap, level_cap, true, shadow);
         if (e != hipSuccess) break;
         WArgs W = wf.args;
         W.ns = ns;
-        W.group = 1;
-        if (ns > 1 && ns <= 64)
-            while (W.group < ns) W.group *= 2;
+        W.group = group;
         W.chain = chain ? 1 : 0;
         W.pool = pool;
         W.level_cap = level_cap;

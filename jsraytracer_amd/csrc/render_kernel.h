@@ -54,6 +54,11 @@ struct WArgs {
     float4 *hand;      // [k * hstride + h], k < 7: shadow hand-off of a lit node (h: path / level index)
     float *root;       // tree: [3 * path] root colours
     uint32_t *lvl;     // tree: [L] ray count of level L; [LVL_FLAG] overflow flag
+    // persistent casts (SDF scenes, render.hip k_extend_q / k_shadow_*): work counters per level
+    // ([L] extend, [32 + L] shadow) and the shadow rays of the light samples ([e] = k_shadow lane e)
+    uint32_t *qctr;
+    float4 *sray;      // [e] {P.xyz, -}, [sstride + e] {delta.xyz, -}
+    float4 *scol;      // [e] {unshadowed colour.xyz, state: 0 no cast / lit, 1 cast pending, 2 shadowed}
     // batch
     uint32_t p0, npix, s0, npaths;
     int32_t ns;        // light samples per lit node
@@ -62,6 +67,7 @@ struct WArgs {
     int32_t pad;
     size_t pool, level_cap;
     size_t nstride, hstride;  // plane strides of child / slot and of hand
+    size_t sstride;           // entries of sray / scol (0: persistent casts not used)
 };
 
 struct Wavefront {  // owns the batch buffers (cached per scene)
@@ -72,7 +78,8 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     size_t cap_bytes = 0;
     WArgs args{};
     // rays: ray slots; nodes: node records; hands: hand-off records; paths: root colours
-    hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree);
+    // shadow: light-sample entries of the persistent shadow casts (0 if unused)
+    hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree, size_t shadow = 0);
     ~Wavefront();
 };
 

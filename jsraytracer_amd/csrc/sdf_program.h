@@ -41,9 +41,11 @@ struct SdfInsn {
     int32_t op, a, b, pad;
 };
 
-constexpr int SDF_MAX_D = 16;   // distance stack depth
-constexpr int SDF_MAX_P = 8;    // point stack depth
-constexpr int SDF_MAX_S = 8;    // scale stack depth
-constexpr int SDF_MAX_LOOP = 4; // nested loops
+// Stack limits sized to the reference scenes (deepest: SDF_Menger d=5, Sierpinski s=3, one loop),
+// small enough for the device VM to keep every stack in registers (the host rejects deeper trees).
+constexpr int SDF_MAX_D = 6;    // distance stack depth
+constexpr int SDF_MAX_P = 2;    // point stack depth
+constexpr int SDF_MAX_S = 4;    // scale stack depth
+constexpr int SDF_MAX_LOOP = 2; // nested loops
 
 }  // namespace jsrt
