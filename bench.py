@@ -8,7 +8,7 @@ columns are dealt to ranks in 16-column blocks (jsraytracer_amd/tiles.py), each 
 tile, and the step ends with one gather of the tiles to rank 0 (RCCL over xGMI, nccl backend) plus the
 permute into image order — strong scaling of one fixed frame.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config cornell_box_path|bunny|SDF_Menger|ASimpleScene]
+    python bench.py [--gpus N --steps K --warmup W] [--config cornell_box_path|bunny|SDF_Menger|dragon|ASimpleScene]
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
   roofline      — for the DOMINANT kernel (largest share of render-kernel time): SURVEY.md §8(d)
@@ -34,7 +34,11 @@ CONFIGS = {
     "bunny": ("bunny", 1920, 1080, 16, 1, 4),
     "SDF_Menger": ("SDF_Menger", 1024, 1024, 32, 1, 4),
     "ASimpleScene": ("ASimpleScene", 256, 256, 1, 1, 4),
+    # BASELINE.json configs[4]: the dragon mesh is built natively from its OBJ (include/jsrt_mesh.h) on
+    # the box, since the reference-built blob is ~47 MB; its tree is bit-identical (tests/test_mesh_build.py)
+    "dragon": ("dragon", 4096, 4096, 256, 1, 4),
 }
+MESH_SCENES = ("dragon",)  # loaded as skeleton + OBJ from tests/golden/meshes
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (HBM3E 8 TB/s spec)
 F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
 CLOCK_HZ = 2.4e9            # max clock, MI355X_MICROARCH.md chip table
@@ -160,8 +164,20 @@ def main():
     from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline leg
 
     scene_name, W, H, spp, kind, depth = CONFIGS[args.config]
-    blob = pyoracle.golden_scene(scene_name)
+    t_load = time.perf_counter()
+    if scene_name in MESH_SCENES:
+        meshes = os.path.join(ROOT, "tests", "golden", "meshes")
+        with open(os.path.join(meshes, "topology.json")) as f:
+            topo = json.load(f)[scene_name]
+        import gzip
+        with gzip.open(os.path.join(meshes, topo["skeleton"]), "rb") as f:
+            skel = f.read()
+        blob, _ = jr.load_obj_scene(skel, os.path.join(meshes, topo["obj_fixture"]))
+    else:
+        blob = pyoracle.golden_scene(scene_name)
+    t_build = time.perf_counter() - t_load
     scene = jr.Scene(blob, device=local)
+    t_upload = time.perf_counter() - t_load - t_build
 
     cb = args.col_block if world > 1 else 1
     fg = FrameGather(W, H, rank, world, cb, device=f"cuda:{local}")
@@ -223,6 +239,7 @@ def main():
                        "col_block": cb},
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms_per_step": kernel_ms,
+            "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
             "stages_note": "stage split from one fully-instrumented step after the timed region",
             "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
             "stage_launches_per_step": stage_launches,

@@ -44,6 +44,17 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_v
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_owned_columns",
            "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
+# exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
+MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_free"]
+
+
+class MeshOptions(ctypes.Structure):
+    _fields_ = [("bvh_object", ctypes.c_int32), ("pad", ctypes.c_int32), ("min_area", ctypes.c_double)]
+
+
+class MeshInfo(ctypes.Structure):
+    _fields_ = [("triangles", ctypes.c_int64), ("nodes", ctypes.c_int64), ("max_depth", ctypes.c_int32),
+                ("bvh_object", ctypes.c_int32)]
 
 _lib = None
 
@@ -78,6 +89,12 @@ def lib():
     L.jsrt_last_error.restype = ctypes.c_char_p
     L.jsrt_abi_version.restype = ctypes.c_int32
     L.jsrt_device_count.restype = ctypes.c_int32
+    L.jsrt_blob_attach_obj.restype = ctypes.c_int
+    L.jsrt_blob_attach_obj.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                       ctypes.POINTER(MeshOptions), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(MeshInfo)]
+    L.jsrt_blob_free.restype = None
+    L.jsrt_blob_free.argtypes = [ctypes.c_void_p]
     _lib = L
     return L
 

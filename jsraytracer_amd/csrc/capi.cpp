@@ -25,6 +25,14 @@ int set_error(int code, const std::string &m) {
     g_err = m;
     return code;
 }
+}  // namespace
+
+namespace jsrt {
+// shared with mesh_build.cpp: the one jsrt_last_error() message per thread
+int record_error(int code, const std::string &m) { return set_error(code, m); }
+}  // namespace jsrt
+
+namespace {
 #define HIP_TRY(expr)                                                                      \
     do {                                                                                   \
         hipError_t e_ = (expr);                                                            \

@@ -1,0 +1,75 @@
+"""TEST INFRASTRUCTURE: read JSRT blob sections and digest a BVHAggregate's tree.
+
+The digest walks the tree the way the reference's exporter and traversal see it (pre-order, lesser
+subtree first, aggregates.js:65-87,221-222) and hashes, per node: depth, leaf flag, AABB centre and
+half size (f32 bit patterns); per leaf object: the Triangle record fields the reference computes
+(geometry.js:335-354: ps, v0, v1, normal, delta, d00, d11, d01, denom, area, vertex normals, UVs),
+the material index and the shadow flag.  Two blobs with equal digests hold bit-identical trees, so
+closest-hit ties break alike.  Record indices (which differ between exporters) are not hashed.
+"""
+import hashlib
+import struct
+
+import numpy as np
+
+TAGS = {"OBJS": 32, "BVHN": 64, "TRIS": 256, "GEOM": 48, "CHLD": 4, "MATS": 256}
+
+
+def fourcc(s):
+    return s[0] | (s[1] << 8) | (s[2] << 16) | (s[3] << 24)
+
+
+def sections(blob):
+    blob = bytes(blob)
+    magic, version, n, _ = struct.unpack_from("<4I", blob, 0)
+    assert magic == 0x5452534A and version == 1, "not a JSRT v1 blob"
+    out = {}
+    for i in range(n):
+        tag, count, off, nbytes = struct.unpack_from("<IIQQ", blob, 16 + 24 * i)
+        name = struct.pack("<I", tag).decode()
+        out[name] = (count, blob[off:off + nbytes])
+    return out
+
+
+def objects(sec):
+    cnt, raw = sec["OBJS"]
+    return np.frombuffer(raw, np.int32).reshape(cnt, 8)  # kind geometry material casts first n bvh_root matrix
+
+
+def bvh_objects(blob):
+    o = objects(sections(blob))
+    return [i for i in range(len(o)) if o[i, 0] == 3]
+
+
+def digest(blob, bvh_object=None):
+    """(sha256 hex, nodes, max_depth, triangles) of a BVHAggregate's tree."""
+    sec = sections(blob)
+    O = objects(sec)
+    if bvh_object is None:
+        bvh_object = [i for i in range(len(O)) if O[i, 0] == 3][0]
+    N = sec["BVHN"][1]
+    C = np.frombuffer(sec["CHLD"][1], np.int32)
+    G = np.frombuffer(sec["GEOM"][1], np.int32).reshape(-1, 12)
+    T = sec["TRIS"][1]
+    h = hashlib.sha256()
+    nodes = tris = maxd = 0
+    stack = [int(O[bvh_object, 6])]
+    while stack:
+        k = stack.pop()
+        rec = N[64 * k:64 * k + 64]
+        center, half = rec[0:16], rec[16:32]
+        is_leaf, lesser, greater, first, n, depth = struct.unpack_from("<I5i", rec, 32)
+        h.update(struct.pack("<iI", depth, is_leaf) + center + half)
+        nodes += 1
+        maxd = max(maxd, depth)
+        if is_leaf:
+            for c in C[first:first + n]:
+                kind, geom, mat, casts = (int(x) for x in O[c, :4])
+                assert kind == 1 and G[geom, 0] == 7, "BVH leaf object is not a Primitive over a Triangle"
+                t = int(G[geom, 1])
+                h.update(struct.pack("<iI", mat, casts) + T[256 * t:256 * t + 256])
+                tris += 1
+        else:
+            stack.append(greater)  # pre-order, lesser first
+            stack.append(lesser)
+    return h.hexdigest(), nodes, maxd, tris

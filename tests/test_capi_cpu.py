@@ -28,7 +28,9 @@ def test_header_symbols_exported(lib):
     declared = _declared("jsrt.h")
     assert set(declared) == set(_native.EXPORTS)
     out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
-    for sym in declared:
+    mesh = _declared("jsrt_mesh.h")
+    assert set(mesh) == set(_native.MESH_EXPORTS)
+    for sym in declared + mesh:
         assert re.search(rf"\bT {sym}$", out, re.M), f"{sym} not exported"
         assert hasattr(lib, sym)
 
