@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--col-block", type=int, default=16)
     ap.add_argument("--no-events", action="store_true", help="A/B: time steps without per-launch HIP events")
+    ap.add_argument("--spp", type=int, default=0, help="profiling only: override the config's spp (same launch "
+                    "shapes, fewer batches); a bench line with it is not the config's number")
     args = ap.parse_args()
 
     rank, world, local = env_int("RANK", 0), env_int("WORLD_SIZE", 1), env_int("LOCAL_RANK", 0)
@@ -164,6 +166,8 @@ def main():
     from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline leg
 
     scene_name, W, H, spp, kind, depth = CONFIGS[args.config]
+    if args.spp > 0:
+        spp = args.spp
     t_load = time.perf_counter()
     if scene_name in MESH_SCENES:
         meshes = os.path.join(ROOT, "tests", "golden", "meshes")
@@ -240,6 +244,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms_per_step": kernel_ms,
             "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
+            "events_lost": {"timed": sum(x["events_lost"] for x in stats), "stage_split": st_after["events_lost"]},
+            "frame_attempts": [x["attempts"] for x in stats],
             "stages_note": "stage split from one fully-instrumented step after the timed region",
             "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
             "stage_launches_per_step": stage_launches,

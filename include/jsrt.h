@@ -58,7 +58,7 @@ typedef struct {
     double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, resolve */
     uint32_t stage_launches[JSRT_STAGES];
     uint32_t attempts;       /* frame attempts: > 1 when a pool / launch bound was outgrown and the frame redone */
-    uint32_t pad;
+    uint32_t events_lost;    /* event pairs whose elapsed time HIP could not report (not in stage_ms) */
 } jsrt_stats;
 
 typedef void (*jsrt_progress_fn)(int32_t pass, double completion, void *user);

@@ -29,14 +29,14 @@ STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("samples", ctypes.c_uint64),
                 ("launches", ctypes.c_uint32), ("batches", ctypes.c_uint32), ("stage_ms", ctypes.c_double * 8),
-                ("stage_launches", ctypes.c_uint32 * 8), ("attempts", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("stage_launches", ctypes.c_uint32 * 8), ("attempts", ctypes.c_uint32), ("events_lost", ctypes.c_uint32)]
 
     def as_dict(self):
         return {"kernel_ms": self.kernel_ms, "total_ms": self.total_ms, "samples": int(self.samples),
                 "launches": int(self.launches), "batches": int(self.batches),
                 "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(8)},
                 "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(8)},
-                "attempts": int(self.attempts)}
+                "attempts": int(self.attempts), "events_lost": int(self.events_lost)}
 
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)

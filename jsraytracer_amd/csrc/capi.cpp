@@ -250,7 +250,7 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
         double ms = 0;
         uint32_t launches = 0;
         for (int k = 0; k < KT_N && k < JSRT_STAGES; ++k) {
-            st->stage_ms[k] = kt.ev[k].total_ms();
+            st->stage_ms[k] = kt.ev[k].total_ms(&st->events_lost);
             st->stage_launches[k] = (uint32_t)kt.ev[k].used;
             ms += st->stage_ms[k];
             launches += (uint32_t)kt.ev[k].used;

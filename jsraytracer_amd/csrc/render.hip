@@ -878,11 +878,12 @@ void EventPairs::begin(hipStream_t s) {
     (void)hipEventRecord(b[used], s);
 }
 void EventPairs::end(hipStream_t s) { (void)hipEventRecord(e[used++], s); }
-double EventPairs::total_ms() const {
+double EventPairs::total_ms(uint32_t *lost) const {
     double ms = 0;
     for (size_t k = 0; k < used; ++k) {
         float x = 0;
         if (hipEventElapsedTime(&x, b[k], e[k]) == hipSuccess) ms += x;
+        else if (lost) ++*lost;
     }
     return ms;
 }
@@ -1103,11 +1104,17 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 if ((e = hipGetLastError()) != hipSuccess) break;
                 done += (uint64_t)W.npix * nb;
                 if (kt) ++kt->batches;
-                if (!chain && wf.frac.empty() && !conservative) {  // learn the level counts once
+                if (!chain && ((wf.frac.empty() && !conservative) || conservative)) {
+                    // learn the level counts: from the scene's first batch, or -- when that batch was
+                    // not representative and a frame had to be redone -- as the maximum over every
+                    // batch of the conservative redo, so later frames of this shape are not redone
                     if ((e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
                     if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                    if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER])
-                        for (int L = 0; L < A.max_depth; ++L) wf.frac.push_back((double)h_lvl[L] / (double)W.npaths);
+                    if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) {
+                        if (wf.frac.size() < (size_t)A.max_depth) wf.frac.assign(A.max_depth, 0.0);
+                        for (int L = 0; L < A.max_depth; ++L)
+                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[L] / (double)W.npaths);
+                    }
                 }
             }
             if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
@@ -1123,7 +1130,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             if (paths * wf.pool_factor > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
             wf.pool_factor *= 2;
             wf.frac.clear();
-        } else {  // a level outgrew its learned bound: redo with the conservative bounds
+        } else {  // a level outgrew its learned bound: redo with the conservative bounds (and relearn)
             conservative = true;
             wf.frac.clear();
         }

@@ -91,7 +91,7 @@ struct EventPairs {  // reusable HIP events bracketing every launch of one kerne
     size_t used = 0;
     void begin(hipStream_t s);
     void end(hipStream_t s);
-    double total_ms() const;  // after the stream is synchronized
+    double total_ms(uint32_t *lost = nullptr) const;  // after the stream is synchronized; lost: pairs without a time
     ~EventPairs();
 };
 
