@@ -141,6 +141,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.sample_call = (const int32_t *)(b + o_sc);
     D.light_draws = H.light_draws;
     D.max_children = H.max_children;
+    D.bvh_stack = H.bvh.empty() ? 0 : H.bvh_max_depth + 2;
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);

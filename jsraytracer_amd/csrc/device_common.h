@@ -543,11 +543,19 @@ template <int PF, bool ANY>
 __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, I.ctx};
     const bool fast = I.count != 0;
-    int stack[64];
+    // Traversal stack in LDS, one column per lane ([entry * blockDim + lane]: lanes at the same depth
+    // hit distinct banks): S.bvh_stack entries (deepest node + 2 >= the D + 1 a greater-first
+    // traversal can hold) of the launch's dynamic LDS (bvh_lds_bytes).  A per-lane array would live
+    // in scratch, and every push/pop would be a memory round trip on the traversal's critical path.
+    extern __shared__ int bvh_lds_stack[];
+    int *const stack = bvh_lds_stack + threadIdx.x;
+    const int stride = (int)blockDim.x;
     int sp = 0;
-    stack[sp++] = I.first;
+    stack[0] = I.first;
+    ++sp;
     while (sp > 0) {
-        const DBvhNode N = S.bvh[stack[--sp]];
+        --sp;
+        const DBvhNode N = S.bvh[stack[sp * stride]];
         double tmn, tmx;
         if (aabb_slab(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, d, minD, maxD, tmn, tmx) && tmn <= maxD && tmx >= minD &&
             tmn <= best.t) {
@@ -564,8 +572,9 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                     }
                 }
             } else {
-                stack[sp++] = N.a;  // lesser, visited after the greater subtree
-                stack[sp++] = N.b;
+                stack[sp * stride] = N.a;  // lesser, visited after the greater subtree
+                stack[(sp + 1) * stride] = N.b;
+                sp += 2;
             }
         }
     }

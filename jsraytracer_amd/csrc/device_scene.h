@@ -145,7 +145,8 @@ struct DScene {
     const int32_t *sample_call;   // ... and the RNG call index of its first draw
     int32_t light_draws;     // RNG draws of all light samples of a node (scatter draws follow)
     int32_t max_children;    // most children one ray-tree node can spawn (0..2)
-    int32_t pad[2];
+    int32_t bvh_stack;       // LDS traversal-stack entries per lane (deepest BVH node + 2; 0: no BVH)
+    int32_t pad;
 };
 
 }  // namespace jsrt

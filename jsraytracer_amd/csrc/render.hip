@@ -969,6 +969,8 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         launch();
         if (ev) kt->ev[which].end(st);
     };
+    // dynamic LDS of the casting kernels: the BVH traversal stack (bvh_cast), 256 lanes x entries
+    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? (size_t)S.bvh_stack * 256 * sizeof(int) : 0;
     // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
     const bool Q = (PF & PF_SDF) && W.sstride != 0;
     if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
@@ -983,7 +985,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 hipLaunchKernelGGL((k_extend_q<PF, CHAIN>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN>, ub)),
                                    dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
             else
-                hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
+                hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
@@ -997,9 +999,9 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                                        dim3(256), 0, st, S, W, L);
                     hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
                 } else if (W.ns <= 64)
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), 0, st, S, W, L);
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
                 else
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L);
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
             });
     }
     if (CHAIN) {

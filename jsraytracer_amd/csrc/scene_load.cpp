@@ -363,6 +363,7 @@ struct Loader {
         int32_t idx = (int32_t)S.bvh.size();
         S.bvh.push_back(DBvhNode{});
         S.n_bvh_nodes++;
+        S.bvh_max_depth = std::max(S.bvh_max_depth, depth);
         DBvhNode d;
         d.cx = R.center[0]; d.cy = R.center[1]; d.cz = R.center[2];
         d.hx = R.half[0]; d.hy = R.half[1]; d.hz = R.half[2];

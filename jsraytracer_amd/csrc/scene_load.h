@@ -42,6 +42,7 @@ struct HostScene {
     int32_t features = 0, profile = PF_ALL;  // PF_* bits used / kernel instantiation chosen
     // workload facts used for algorithmic-byte accounting
     int64_t n_bvh_nodes = 0, n_triangles = 0;
+    int32_t bvh_max_depth = 0;  // deepest BVH node (root = 0): sizes the LDS traversal stack
 };
 
 // Returns 0 on success; otherwise fills err.
