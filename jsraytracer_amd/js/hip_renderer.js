@@ -107,4 +107,9 @@ class NodePixelBuffer {
     coord(x, y) { return y * (this.imgdata.width * 4) + x * 4; }
 }
 
-module.exports = { HipRenderer, NodePixelBuffer, addon, readHeader };
+// loadObjFile(...) + BVHAggregate.build(...) natively (include/jsrt_mesh.h): splices the OBJ's triangles
+// and their reference-identical BVH into the skeleton blob's one-leaf BVHAggregate (its template
+// Primitive carries the material and transform loadObjFile would be given).
+function attachObj(blob, objText, opts) { return addon().attachObj(blob, objText, opts || {}); }
+
+module.exports = { HipRenderer, NodePixelBuffer, addon, readHeader, attachObj };

@@ -22,6 +22,7 @@
 #include <string>
 
 #include "../../include/jsrt.h"
+#include "../../include/jsrt_mesh.h"
 
 namespace {
 
@@ -310,6 +311,69 @@ napi_value Render(napi_env env, napi_callback_info info) {
     return promise;
 }
 
+// attachObj(blob, objText, {bvhObject, minArea}?) -> {blob: Buffer, triangles, nodes, maxDepth}
+// loadObjFile + BVHAggregate.build natively (include/jsrt_mesh.h; objloader.js:224-231, aggregates.js:33-41)
+napi_value AttachObj(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    void *data = nullptr;
+    size_t len = 0;
+    if (argc < 2 || !get_bytes(env, argv[0], &data, &len)) {
+        napi_throw_type_error(env, "JSRT", "attachObj(blob: Uint8Array, objText: string | Uint8Array, opts?)");
+        return nullptr;
+    }
+    std::string text;
+    void *tb = nullptr;
+    size_t tl = 0;
+    if (get_bytes(env, argv[1], &tb, &tl)) {
+        text.assign((const char *)tb, tl);
+    } else {
+        size_t n = 0;
+        if (napi_get_value_string_utf8(env, argv[1], nullptr, 0, &n) != napi_ok) {
+            napi_throw_type_error(env, "JSRT", "attachObj: objText must be a string or Uint8Array");
+            return nullptr;
+        }
+        text.resize(n + 1);
+        napi_get_value_string_utf8(env, argv[1], &text[0], n + 1, &n);
+        text.resize(n);
+    }
+    jsrt_mesh_options opt{-1, 0, 0.00001};
+    if (argc > 2) {
+        napi_valuetype t;
+        napi_typeof(env, argv[2], &t);
+        if (t == napi_object) {
+            napi_value v;
+            bool has = false;
+            if (napi_has_named_property(env, argv[2], "bvhObject", &has) == napi_ok && has &&
+                napi_get_named_property(env, argv[2], "bvhObject", &v) == napi_ok)
+                napi_get_value_int32(env, v, &opt.bvh_object);
+            if (napi_has_named_property(env, argv[2], "minArea", &has) == napi_ok && has &&
+                napi_get_named_property(env, argv[2], "minArea", &v) == napi_ok)
+                napi_get_value_double(env, v, &opt.min_area);
+        }
+    }
+    void *out = nullptr;
+    size_t out_n = 0;
+    jsrt_mesh_info mi;
+    if (jsrt_blob_attach_obj(data, len, text.data(), text.size(), &opt, &out, &out_n, &mi) != 0)
+        return throw_jsrt(env, "jsrt_blob_attach_obj");
+    napi_value buf, o, v;
+    void *dst = nullptr;
+    napi_status st = napi_create_buffer_copy(env, out_n, out, &dst, &buf);
+    jsrt_blob_free(out);
+    NAPI_OK(st);
+    NAPI_OK(napi_create_object(env, &o));
+    napi_set_named_property(env, o, "blob", buf);
+    napi_create_double(env, (double)mi.triangles, &v);
+    napi_set_named_property(env, o, "triangles", v);
+    napi_create_double(env, (double)mi.nodes, &v);
+    napi_set_named_property(env, o, "nodes", v);
+    napi_create_int32(env, mi.max_depth, &v);
+    napi_set_named_property(env, o, "maxDepth", v);
+    return o;
+}
+
 napi_value DeviceCount(napi_env env, napi_callback_info) {
     napi_value v;
     napi_create_int32(env, jsrt_device_count(), &v);
@@ -342,6 +406,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, AbiVersion, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"ownedColumns", nullptr, OwnedColumns, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"attachObj", nullptr, AttachObj, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

@@ -42,8 +42,34 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     keys, nums = r.stdout.strip().split("\n")
     assert json.loads(keys) == sorted(["sceneCreate", "sceneDestroy", "renderSync", "render", "deviceCount",
-                                       "abiVersion", "ownedColumns"])
+                                       "abiVersion", "ownedColumns", "attachObj"])
     assert nums.split() == ["1", "16", "3"]
+
+
+def test_addon_attach_obj_matches_python_and_reference(addon, tmp_path):
+    """attachObj (loadObjFile + BVHAggregate.build, natively) from node: the same blob bytes as the
+    Python binding, and the bunny tree equals the reference's (tests/test_mesh_build.py digest)."""
+    import gzip
+
+    import jsraytracer_amd as jr
+    import mesh_topology as mt
+    meshes = os.path.join(ROOT, "tests", "golden", "meshes")
+    out = tmp_path / "bunny.jsrt"
+    code = (f"const a=require({json.dumps(addon)}); const z=require('zlib'), fs=require('fs');"
+            f"const skel=z.gunzipSync(fs.readFileSync({json.dumps(os.path.join(meshes, 'bunny.skel.jsrt.gz'))}));"
+            f"const obj=z.gunzipSync(fs.readFileSync({json.dumps(os.path.join(meshes, 'bunny2.obj.gz'))})).toString();"
+            "const r=a.attachObj(skel, obj, {minArea: 0.00001});"
+            f"fs.writeFileSync({json.dumps(str(out))}, r.blob); console.log(r.triangles, r.nodes, r.maxDepth);"
+            "try { a.attachObj(skel, 'v 0 0 0\\nbogus\\n'); console.log('no throw'); } catch (e) { console.log(e.message); }")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert lines[0].split() == ["4968", "9935", "15"]
+    assert lines[1].startswith("jsrt_blob_attach_obj: Error while attempting to parse obj file")
+    with gzip.open(os.path.join(meshes, "bunny.skel.jsrt.gz"), "rb") as f:
+        py, _ = jr.attach_obj(f.read(), jr.mesh.read_obj(os.path.join(meshes, "bunny2.obj.gz")))
+    assert out.read_bytes() == py
+    assert mt.digest(py) == mt.digest(pyoracle.golden_scene("bunny"))
 
 
 def test_addon_errors_are_thrown(addon):
