@@ -31,11 +31,15 @@
 #ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade (register budget)
 #define JSRT_SHADE_OCC 2
 #endif
+// k_shadow / k_extend: at least 6 / 5 waves per SIMD.  Their casts are latency-bound (BVH node and
+// scene loads on a dependent chain), so more resident waves beat the registers the compiler would
+// otherwise keep (A/B on MI355X: cornell +3 %, bunny +15 %, dragon +4 % against no bound; 8 waves
+// for k_shadow spills and loses 11 % on cornell).
 #ifndef JSRT_SHADOW_OCC
-#define JSRT_SHADOW_OCC 1
+#define JSRT_SHADOW_OCC 6
 #endif
 #ifndef JSRT_EXTEND_OCC
-#define JSRT_EXTEND_OCC 1
+#define JSRT_EXTEND_OCC 5
 #endif
 // optional waves-per-EU window (min, max) per kernel for A/B occupancy experiments
 #ifdef JSRT_SHADOW_WPE
