@@ -69,7 +69,9 @@ void jsrt_scene_destroy(jsrt_scene *scene);
 
 /* Render into host buffers.  rgba8 (W*H*4 bytes) receives the PixelBuffer bytes of the rendered
  * columns only (other columns untouched, as each reference worker leaves them); colors_f32
- * (W*H*4, nullable) the final f32 colour handed to setColor (alpha 1).  progress may be NULL. */
+ * (W*H*4, nullable) the final f32 colour handed to setColor (alpha 1).  progress may be NULL.
+ * Incremental renderer with progress: before each callback for pass p, rgba8's owned columns hold
+ * the running mean of samples 0..p (the img the reference's callback sees, renderers.js:93-112). */
 int jsrt_render(jsrt_scene *scene, const jsrt_params *params, uint8_t *rgba8, float *colors_f32,
                 jsrt_progress_fn progress, void *user, jsrt_stats *stats);
 

@@ -210,8 +210,26 @@ int resolve(const jsrt_scene *s, const jsrt_params *p, int32_t col_block, Resolv
 
 // Renders one frame (all spp) on `stream` through the wavefront schedule (render.hip); every
 // kernel launch is bracketed by HIP events recorded on that same stream.
+// Owned column c, row py -> image (px, py) of the host PixelBuffer; other columns untouched
+// (worker.js semantics).
+void scatter_columns(const RenderArgs &a, const uint32_t *h_rgba, const float *h_col, uint8_t *rgba8,
+                     float *colors_f32) {
+    for (int32_t c = 0; c < a.ncols; ++c) {
+        const int32_t px = owned_to_px(c, a.x_offset, a.x_delt, 1);
+        for (int32_t py = 0; py < a.H; ++py) {
+            const size_t src = (size_t)c * a.H + py, dst = (size_t)py * a.W + px;
+            memcpy(rgba8 + 4 * dst, &h_rgba[src], 4);
+            if (colors_f32 && h_col) memcpy(colors_f32 + 4 * dst, &h_col[4 * src], 16);
+        }
+    }
+}
+
+// host_rgba (nullable): the caller's PixelBuffer.  With a progress callback and the Incremental
+// renderer, the running mean of the passes done so far is written into its owned columns before each
+// callback (renderers.js:93-112: setColor every pass, callback reads img), from clean passes only.
 int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_rgba, float *d_colors,
-                 hipStream_t stream, jsrt_progress_fn progress, void *user, jsrt_stats *st) {
+                 hipStream_t stream, jsrt_progress_fn progress, void *user, jsrt_stats *st,
+                 uint8_t *host_rgba = nullptr) {
     const size_t nacc = (size_t)a.ncols * a.H * 4;
     float *accum = nullptr;
     HIP_TRY(hipMallocAsync((void **)&accum, nacc * sizeof(float) + 16, stream));
@@ -230,13 +248,28 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     if (p && p->stage_events) kt.mask = (uint32_t)p->stage_events;
     auto t_last = std::chrono::steady_clock::now();
     const double tl = p ? p->timelimit_ms : 0;
-    std::function<bool(int, double)> prog;
+    a.samples_per_batch = (p && p->samples_per_launch > 0) ? p->samples_per_launch : 0;
+    const bool preview = host_rgba && a.kind == JSRT_RENDERER_INCREMENTAL;
+    std::vector<uint32_t> h_prev;
+    std::function<bool(int, double, bool)> prog;
+    int prev_rc = 0;
     if (progress && tl > 0)
-        prog = [&](int pass, double completion) {  // renderers.js:103-112 cadence, at batch granularity
+        prog = [&](int pass, double completion, bool clean) {  // renderers.js:103-112 cadence, batch granularity
             if (completion >= 1.0) return true;
             auto now = std::chrono::steady_clock::now();
             if (std::chrono::duration<double, std::milli>(now - t_last).count() >= tl) {
                 t_last = now;
+                if (preview && clean) {
+                    const size_t npx = (size_t)a.ncols * a.H;
+                    h_prev.resize(npx);
+                    if (render_preview(a, pass + 1, stream) != hipSuccess ||
+                        hipMemcpyAsync(h_prev.data(), d_rgba, npx * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                        hipStreamSynchronize(stream) != hipSuccess) {
+                        prev_rc = set_error(-3, "progress preview failed");
+                        return false;
+                    }
+                    scatter_columns(a, h_prev.data(), nullptr, host_rgba, nullptr);
+                }
                 progress(pass, completion, user);
             }
             return true;
@@ -244,8 +277,8 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : (size_t)2 << 20;
     if (const char *e = getenv("JSRT_MAX_PATHS")) max_paths = (size_t)atoll(e);
     hipError_t e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
-    int rc = 0;
-    if (e != hipSuccess) rc = set_error(-3, std::string("render: ") + hipGetErrorString(e));
+    int rc = prev_rc;
+    if (!rc && e != hipSuccess) rc = set_error(-3, std::string("render: ") + hipGetErrorString(e));
     if (!rc && st) {
         if (hipStreamSynchronize(stream) != hipSuccess) rc = set_error(-3, "render kernels failed");
         double ms = 0;
@@ -288,7 +321,7 @@ int jsrt_render(jsrt_scene *s, const jsrt_params *p, uint8_t *rgba8, float *colo
     memset(&st, 0, sizeof st);
     if (hipMalloc(&d_rgba, npx * 4) != hipSuccess) rc = set_error(-3, "out of device memory");
     if (!rc && colors_f32 && hipMalloc(&d_col, npx * 16) != hipSuccess) rc = set_error(-3, "out of device memory");
-    if (!rc) rc = run_launches(s, p, a, d_rgba, d_col, stream, progress, user, &st);
+    if (!rc) rc = run_launches(s, p, a, d_rgba, d_col, stream, progress, user, &st, rgba8);
     if (!rc && npx) {
         std::vector<uint32_t> h_rgba(npx);
         std::vector<float> h_col(colors_f32 ? npx * 4 : 0);
@@ -296,16 +329,7 @@ int jsrt_render(jsrt_scene *s, const jsrt_params *p, uint8_t *rgba8, float *colo
             (colors_f32 && hipMemcpyAsync(h_col.data(), d_col, npx * 16, hipMemcpyDeviceToHost, stream) != hipSuccess) ||
             hipStreamSynchronize(stream) != hipSuccess)
             rc = set_error(-3, "device-to-host copy failed");
-        if (!rc) {  // owned column c, row py -> image (px, py); other columns untouched (worker.js semantics)
-            for (int32_t c = 0; c < a.ncols; ++c) {
-                const int32_t px = owned_to_px(c, a.x_offset, a.x_delt, 1);
-                for (int32_t py = 0; py < a.H; ++py) {
-                    const size_t src = (size_t)c * a.H + py, dst = (size_t)py * a.W + px;
-                    memcpy(rgba8 + 4 * dst, &h_rgba[src], 4);
-                    if (colors_f32) memcpy(colors_f32 + 4 * dst, &h_col[4 * src], 16);
-                }
-            }
-        }
+        if (!rc) scatter_columns(a, h_rgba.data(), colors_f32 ? h_col.data() : nullptr, rgba8, colors_f32);
     }
     if (d_rgba) (void)hipFree(d_rgba);
     if (d_col) (void)hipFree(d_col);

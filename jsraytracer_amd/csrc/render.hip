@@ -843,11 +843,11 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
     A.accum[4 * oi + 2] = acc.z;
 }
 
-__global__ __launch_bounds__(256) void k_final(RenderArgs A) {
+__global__ __launch_bounds__(256) void k_final(RenderArgs A, int32_t passes) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= (uint32_t)A.ncols * A.H) return;
     const F3 acc = f3(A.accum[4 * p], A.accum[4 * p + 1], A.accum[4 * p + 2]);
-    const F3 out = (A.kind == JSRT_RENDERER_INCREMENTAL) ? scale(acc, 1.0 / A.spp) : acc;  // times(1/(iter+1))
+    const F3 out = (A.kind == JSRT_RENDERER_INCREMENTAL) ? scale(acc, 1.0 / passes) : acc;  // times(1/(iter+1))
     A.rgba[p] = set_color_rgba(out);
     if (A.colors) {
         A.colors[4 * p] = out.x;
@@ -1030,7 +1030,7 @@ void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStrea
 }  // namespace
 
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
-                        size_t max_paths, const std::function<bool(int, double)> &progress) {
+                        size_t max_paths, const std::function<bool(int, double, bool)> &progress) {
     if (!A.accum) return hipErrorInvalidValue;
     const uint32_t npix_total = (uint32_t)A.patches * 64u;
     if (ns > 4) max_paths = max_paths * 4 / (size_t)ns;  // the per-sample hand-off scales with ns
@@ -1038,6 +1038,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     uint32_t npix = npix_total, nsb = 1;  // batch: [p0, p0 + npix) pixels x [s0, s0 + nsb) samples
     if ((size_t)npix > max_paths) npix = (uint32_t)(max_paths & ~(size_t)63);
     else nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)A.spp));
+    if (A.samples_per_batch > 0) nsb = std::min<uint32_t>(nsb, (uint32_t)A.samples_per_batch);
     // Chain schedule when no node can have two children: depth x paths node records, nothing can
     // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all
     // levels of a batch (one level may hold half of it), compacted level by level.  Its launches
@@ -1124,8 +1125,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 }
             }
             if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
+                if (!chain && (e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
                 if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                stop = !progress((int)(s0 + nb - 1), (double)done / (double)total);
+                const bool clean = chain || (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]);
+                stop = !progress((int)(s0 + nb - 1), (double)done / (double)total, clean);
             }
         }
         if (e != hipSuccess || chain) break;
@@ -1146,8 +1149,15 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     if (e != hipSuccess) return e;
     const bool ev = kt && kt->on(KT_FINAL);
     if (ev) kt->ev[KT_FINAL].begin(st);
-    hipLaunchKernelGGL(k_final, dim3(grid((size_t)A.ncols * A.H)), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(k_final, dim3(grid((size_t)A.ncols * A.H)), dim3(256), 0, st, A, (int32_t)A.spp);
     if (ev) kt->ev[KT_FINAL].end(st);
+    return hipGetLastError();
+}
+
+hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st) {
+    if (!A.accum || !A.rgba || passes < 1) return hipErrorInvalidValue;
+    if ((size_t)A.ncols * A.H == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_final, dim3(grid((size_t)A.ncols * A.H)), dim3(256), 0, st, A, (int32_t)passes);
     return hipGetLastError();
 }
 

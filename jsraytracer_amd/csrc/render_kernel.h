@@ -25,7 +25,7 @@ struct RenderArgs {
     int32_t final_pass;
     int32_t patches_x; // ceil(ncols / 8)
     int32_t patches;   // patches_x * ceil(H / 8)
-    int32_t pad;
+    int32_t samples_per_batch;  // progress granularity: cap on samples per batch (<= 0: none)
 };
 
 // node info bits (k_shade -> k_shadow / k_reduce / k_resolve)
@@ -109,9 +109,15 @@ struct KernelTimes {
 
 // Renders all spp samples of the owned pixels: A.accum must hold ncols*H*4 floats.
 // `ns` = light samples per lit node (sum over lights; point lights count 1).
-// progress(pass, completion) -> false aborts.
+// progress(pass, completion, clean) -> false aborts.  It is called after samples [0, pass] of every
+// pixel are in A.accum and the stream is idle; clean = no batch so far outgrew its pool / bounds
+// (so the accumulator holds exactly the reference's sums and render_preview may publish it).
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
-                        size_t max_paths, const std::function<bool(int, double)> &progress);
+                        size_t max_paths, const std::function<bool(int, double, bool)> &progress);
+
+// Running mean of the first `passes` samples -> A.rgba / A.colors (k_final with times(1/passes),
+// renderers.js:93-98): the image IncrementalMultisamplingRenderer holds after pass passes-1.
+hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st);
 
 // Owned column c -> image column px (see jsrt.h jsrt_render_device).
 __host__ __device__ inline int32_t owned_to_px(int32_t c, int32_t x_offset, int32_t x_delt, int32_t col_block) {

@@ -115,6 +115,29 @@ def test_gpu_progress_callback(jr):
     assert [c for _, c in seen] == sorted(c for _, c in seen)
 
 
+@pytest.mark.parametrize("scene,W,H,spp,depth,x_offset,x_delt", [
+    ("cornell_box_path", 40, 32, 6, 8, 0, 1),   # chain schedule
+    ("cornell_box_path", 40, 32, 4, 8, 1, 3),   # one worker's columns
+    ("bunny", 32, 24, 4, 4, 0, 1),              # tree schedule (Fresnel children)
+])
+def test_gpu_progress_preview_is_running_mean(jr, scene, W, H, spp, depth, x_offset, x_delt):
+    """renderers.js:93-112: the Incremental renderer setColor()s the running mean every pass, so the
+    img its callback sees after pass p is the frame of the first p+1 samples.  The keyed RNG makes
+    sample k of a pixel independent of spp, so that frame is the spp=p+1 render, bit for bit."""
+    sc = _scene(jr, scene)
+    img = np.zeros((H, W, 4), np.uint8)
+    snaps = {}
+    sc.render(W, H, spp, depth, 1, 5, x_offset, x_delt, samples_per_launch=1, rgba=img, want_colors=False,
+              progress=lambda p, c: snaps.__setitem__(p, img.copy()), timelimit_ms=1e-6)
+    assert sorted(snaps) == list(range(spp - 1))  # every pass but the last, which the final write covers
+    for p, snap in snaps.items():
+        ref = np.zeros((H, W, 4), np.uint8)
+        ref, _, _ = sc.render(W, H, p + 1, depth, 1, 5, x_offset, x_delt, rgba=ref, want_colors=False)
+        assert np.array_equal(snap, ref), f"{scene} pass {p}: {int((snap != ref).any(-1).sum())} pixels differ"
+    final, _, _ = sc.render(W, H, spp, depth, 1, 5, x_offset, x_delt, want_colors=False)
+    assert np.array_equal(img, final)
+
+
 def test_gpu_partition_invariance(jr):
     """renderers.js:88 column interleave: N workers' images composite to the single-worker image."""
     sc = _scene(jr, "cornell_box_path")
