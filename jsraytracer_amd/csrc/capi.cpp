@@ -274,7 +274,10 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
             }
             return true;
         };
-    size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : (size_t)1 << 24;  // 16 M paths: A/B on MI355X vs 2 M: dragon +50 %, Menger x2.5, bunny +18 %, cornell +2 %
+    // default batch (A/B on MI355X, tools/ab_maxpaths.sh): 16 M paths for analytic scenes (cornell: 32 M
+    // loses 1 %), 32 M when the scene holds a BVH, triangles or an SDF (dragon +4 %, Menger +12 % over 16 M)
+    const size_t def_paths = (s->ds.profile & (PF_BVH | PF_TRI | PF_SDF)) ? (size_t)1 << 25 : (size_t)1 << 24;
+    size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : def_paths;
     if (const char *e = getenv("JSRT_MAX_PATHS")) max_paths = (size_t)atoll(e);
     hipError_t e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
     int rc = prev_rc;
