@@ -1,27 +1,39 @@
-"""Benchmark: pixel-samples/s of the HIP renderer on BASELINE.json's headline workload.
+"""Benchmark: pixel-samples/s of the HIP renderer on BASELINE.json's workloads.
 
-Workload (BASELINE.json configs[1]): tests/cornell_box_path, 1024x1024, 64 spp, maxRecursionDepth 8,
-IncrementalMultisamplingRenderer semantics, keyed RNG seed 1 — the reference's own scene graph
+Headline (BASELINE.json configs[1]): tests/cornell_box_path, 1024x1024, 64 spp, maxRecursionDepth 8,
+IncrementalMultisamplingRenderer semantics, keyed RNG seed 1 -- the reference's own scene graph
 (committed as tests/golden/scenes/cornell_box_path.jsrt.gz, exported from the live reference).
-A "step" renders one full frame (all 64 spp of every pixel) into HBM.  With N GPUs the frame's
-columns are dealt to ranks in 16-column blocks (jsraytracer_amd/tiles.py), each rank renders its
-tile, and the step ends with one gather of the tiles to rank 0 (RCCL over xGMI, nccl backend) plus the
-permute into image order — strong scaling of one fixed frame.
+A "step" renders one full frame (all spp of every pixel) into HBM.  With N GPUs the frame's columns
+are dealt to ranks in 16-column blocks (jsraytracer_amd/tiles.py), each rank renders its tile, and
+the step ends with one gather of the tiles to rank 0 (RCCL over xGMI, nccl backend) plus the permute
+into image order -- strong scaling of one fixed frame (the reference's column split across workers,
+src/raytrace_launcher.js:65-101, src/renderers.js:88).
 
     python bench.py [--gpus N --steps K --warmup W] [--config cornell_box_path|bunny|SDF_Menger|dragon|ASimpleScene]
 
+--gpus N > 1 without a torch.distributed environment spawns N rank processes of this script (one per
+GPU, RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on 127.0.0.1) before anything touches a GPU; under
+torchrun the environment is used as given.
+
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
-  roofline      — for the DOMINANT kernel (largest share of render-kernel time): SURVEY.md §8(d)
-                  algorithmic bytes per unit x units per launch / its average launch duration (HIP
-                  events on the render stream, measured live) vs 8 TB/s.  traffic = HBM bytes per launch
-                  from the committed rocprofv3 PMC passes (profiles/pmc_summary.json; FETCH_SIZE
-                  doubled per the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE).  The "valu"
-                  member carries the compute side, which binds for the analytic/SDF scenes.
-  cpu_baseline  — the C oracle (port of the reference path) on a bounded column subsample, host cores.
+  roofline      -- for the DOMINANT kernel (largest share of render-kernel time), against the resource
+                   that binds it: "valu" (scene cache-resident: cornell, bunny, Menger,
+                   ASimpleScene) reports the kernel's f64 TFLOP/s (PMC-counted f64 flops per launch, from
+                   the committed rocprofv3 passes in profiles/pmc_summary.json, over its average launch
+                   duration measured live with HIP events on the render stream) against 78.6 TF, with
+                   the VALU issue fraction and HBM traffic beside it; "hbm" (dragon: 13 MB of BVH and
+                   triangles) reports SURVEY.md §8(d) algorithmic bytes per launch over the same live
+                   duration against 8 TB/s.
+  cpu_baseline  -- the C oracle (port of the reference path) on a bounded column subsample, host cores,
+                   with the reference JS web-worker figure recorded in BASELINE.md beside it.
+  parity        -- the timed frame's columns checked against the oracle's render of the same columns:
+                   RGBA8 bit-exact, f32 colour |d| <= 1e-5 (north_star), at the benchmark's full size.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,23 +41,31 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (scene, W, H, spp, kind, max_depth)
-    "cornell_box_path": ("cornell_box_path", 1024, 1024, 64, 1, 8),
-    "bunny": ("bunny", 1920, 1080, 16, 1, 4),
-    "SDF_Menger": ("SDF_Menger", 1024, 1024, 32, 1, 4),
-    "ASimpleScene": ("ASimpleScene", 256, 256, 1, 1, 4),
+    # name: (scene, W, H, spp, kind, max_depth, binding resource)
+    "cornell_box_path": ("cornell_box_path", 1024, 1024, 64, 1, 8, "valu"),
+    "bunny": ("bunny", 1920, 1080, 16, 1, 4, "valu"),
+    "SDF_Menger": ("SDF_Menger", 1024, 1024, 32, 1, 4, "valu"),
+    "ASimpleScene": ("ASimpleScene", 256, 256, 1, 1, 4, "valu"),
     # BASELINE.json configs[4]: the dragon mesh is built natively from its OBJ (include/jsrt_mesh.h) on
     # the box, since the reference-built blob is ~47 MB; its tree is bit-identical (tests/test_mesh_build.py)
-    "dragon": ("dragon", 4096, 4096, 256, 1, 4),
+    "dragon": ("dragon", 4096, 4096, 256, 1, 4, "hbm"),
 }
+HEADLINE = "cornell_box_path"
+METRIC = "pixel-samples/sec + %HBM-roofline, {scene} {size} @1/2/4/8 GPU"  # BASELINE.json metric, per config
 MESH_SCENES = ("dragon",)  # loaded as skeleton + OBJ from tests/golden/meshes
+# the reference JS web-worker path, measured in the survey container:
+# node 12 worker_threads, 8 workers, column interleave; it cannot run on the GPU box (no reference there)
+REFERENCE_JS = {"cornell_box_path": (10751, "64^2x4spp / 128^2x2spp"), "bunny": (18388, "128^2x1spp"),
+                "dragon": (21816, "128^2x1spp (Incremental forced to 1 spp)"), "SDF_Menger": (3306, "64^2x1spp"),
+                "ASimpleScene": (29627, "128^2x1spp")}
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (HBM3E 8 TB/s spec)
 F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
 CLOCK_HZ = 2.4e9            # max clock, MI355X_MICROARCH.md chip table
 SIMDS = 256 * 4
-# issue cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md: f32 2 cyc; f64 at half
-# the f32 rate; transcendentals 4x)
+# issue cycles per wave64 VALU instruction (MI355X_MICROARCH.md: f32 / int on a SIMD-32 2 cyc; f64 at
+# half the f32 rate 4; transcendentals 4x their type's rate)
 ISSUE_CYC = {"f64": 4.0, "trans_f64": 16.0, "trans_f32": 8.0, "other": 2.0}
+TOL = 1e-5                  # north_star: RGB L-inf on the f32 colour handed to setColor
 
 
 def env_int(name, default):
@@ -53,6 +73,36 @@ def env_int(name, default):
         return int(os.environ.get(name, default))
     except ValueError:
         return default
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """One process per GPU (rank r on device r), started before this process touches a GPU.  Rank 0
+    prints the bench line.  If any rank fails the others are stopped (they would wait in a collective)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def kernel_units(counts, kname):
@@ -71,24 +121,50 @@ def kernel_units(counts, kname):
     return None, None, None
 
 
-def cpu_baseline(blob, W, H, spp, kind, depth, target_s=12.0):
-    """The oracle (C port of the reference path) timed on a bounded column subsample of the same frame."""
+def oracle_columns(blob, W, H, spp, kind, depth, x_offset, x_delt, threads):
     from oracle import pyoracle
+    t = time.time()
+    col, rgba, st = pyoracle.render(blob, W, H, spp, depth, kind, 1, x_offset, x_delt, threads=threads)
+    return col, rgba, st, time.time() - t
+
+
+def cpu_baseline(blob, W, H, spp, kind, depth, target_s=12.0):
+    """The oracle (C port of the reference path) timed on a bounded column subsample of the same frame.
+    Returns the baseline record, per-sample counts, and the oracle's columns (kept for the parity check)."""
     threads = min(16, os.cpu_count() or 1)
     stride = max(1, W // max(threads, 1))  # probe: a thin slice to estimate speed, then size the sample
-    t = time.time()
-    _, _, st = pyoracle.render(blob, W, H, spp, depth, kind, 1, 0, stride, threads=threads)
-    dt = max(time.time() - t, 1e-3)
-    want = st["samples"] / dt * target_s
+    _, _, st, dt = oracle_columns(blob, W, H, spp, kind, depth, 0, stride, threads)
+    want = st["samples"] / max(dt, 1e-3) * target_s
     ncols = int(max(threads, min(W, want / (H * spp))))
     stride = max(1, W // ncols)
-    t = time.time()
-    _, _, st = pyoracle.render(blob, W, H, spp, depth, kind, 1, 0, stride, threads=threads)
-    dt = time.time() - t
+    col, rgba, st, dt = oracle_columns(blob, W, H, spp, kind, depth, 0, stride, threads)
     counts = {k: st[k] / st["samples"] for k in st}
     sample = f"columns px%{stride}==0 of the {W}x{H}x{spp} frame ({st['samples']} pixel-samples, {dt:.1f} s)"
-    return {"value": st["samples"] / dt, "unit": "pixel-samples/s", "cores": threads, "kind": "port",
-            "sample": sample}, counts
+    base = {"value": st["samples"] / dt, "unit": "pixel-samples/s", "cores": threads, "kind": "port",
+            "sample": sample}
+    return base, counts, (col, rgba, 0, stride)
+
+
+def parity(image, colors, ref):
+    """image: [H, W, 4] u8 of the timed frame (rank 0, after the gather); colors: [H, W, 4] f32 or None;
+    ref: (oracle colours, oracle rgba, x_offset, x_delt) of the same frame's columns."""
+    import numpy as np
+    ocol, orgba, x0, dx = ref
+    cols = list(range(x0, image.shape[1], dx))
+    bad = (image[:, cols] != orgba[:, cols]).any(-1)
+    out = {"columns": len(cols), "column_stride": dx, "pixels": int(bad.size), "rgba8_pixels_differing": int(bad.sum()),
+           "rgba8_max_abs": int(np.abs(image[:, cols].astype(int) - orgba[:, cols].astype(int)).max())}
+    if colors is not None:
+        g, o = colors[:, cols, :3], ocol[:, cols, :3]
+        fin = np.isfinite(o)
+        out["f32_max_abs"] = float(np.abs(g[fin] - o[fin]).max()) if fin.any() else 0.0
+        out["f32_nonfinite_pattern_equal"] = bool(np.array_equal(np.isfinite(g), fin))
+        out["f32_bit_exact"] = bool(np.array_equal(g.view(np.uint32), o.view(np.uint32)))
+        out["tolerance"] = TOL
+        out["pass"] = out["rgba8_pixels_differing"] == 0 and out["f32_max_abs"] <= TOL and out["f32_nonfinite_pattern_equal"]
+    else:
+        out["pass"] = out["rgba8_pixels_differing"] == 0
+    return out
 
 
 def load_pmc(config, kname):
@@ -105,25 +181,26 @@ def load_pmc(config, kname):
     return d["kernels"][hits[0]], d.get("source"), hits[0]
 
 
-def roofline(config, dom, avg_ms, launches, counts, samples_per_frame):
-    """dom: the dominant kernel; avg_ms: its average launch duration from the HIP events that
-    bracketed its launches in the timed region (on the render stream)."""
-    kname = dom
+def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
+    """dom: the dominant kernel; avg_ms: its average launch duration from the HIP events that bracketed
+    its launches in the timed region (on the render stream)."""
     per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
-    r = {"bound": "hbm", "kernel": kname, "unit": "GB/s", "peak": HBM_PEAK_GBS, "avg_launch_ms": avg_ms,
-         "launches_per_step": launches, "achieved": None, "frac": None, "traffic": None}
+    r = {"bound": bound, "kernel": dom, "avg_launch_ms": avg_ms, "launches_per_step": launches,
+         "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    sec = avg_ms * 1e-3
     if per_sample:
         units_per_launch = per_sample * samples_per_frame / launches
         per_launch = bpu * units_per_launch
-        r.update(achieved=per_launch / (avg_ms * 1e-3) / 1e9, algorithmic_bytes_per_launch=per_launch,
-                 bytes_per_unit=bpu, work_unit=unit, units_per_launch=units_per_launch)
-        r["frac"] = r["achieved"] / HBM_PEAK_GBS
-    pmc, src, r["kernel"] = load_pmc(config, kname)
+        r["algorithmic"] = {"bytes_per_launch": per_launch, "bytes_per_unit": bpu, "work_unit": unit,
+                            "units_per_launch": units_per_launch, "GBs": per_launch / sec / 1e9,
+                            "frac_of_hbm": per_launch / sec / 1e9 / HBM_PEAK_GBS,
+                            "note": "SURVEY.md §8(d) scene-record bytes; > 1 of HBM means cache-served"}
+    pmc, src, r["kernel"] = load_pmc(config, dom)
     if pmc:
         n = pmc["dispatches"]
-        traffic = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n  # KB -> B, gfx950 x2
+        traffic = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n  # KB -> B, gfx950 x2 on reads
         r["traffic"] = traffic
-        r["traffic_GBs"] = traffic / (avg_ms * 1e-3) / 1e9
+        r["traffic_GBs"] = traffic / sec / 1e9
         r["traffic_frac"] = r["traffic_GBs"] / HBM_PEAK_GBS
         f64 = pmc.get("SQ_INSTS_VALU_ADD_F64", 0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0) + pmc.get("SQ_INSTS_VALU_FMA_F64", 0)
         tr64, tr32 = pmc.get("SQ_INSTS_VALU_TRANS_F64", 0), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0)
@@ -133,10 +210,17 @@ def roofline(config, dom, avg_ms, launches, counts, samples_per_frame):
                  other * ISSUE_CYC["other"]) / n
         flops = (pmc.get("SQ_INSTS_VALU_ADD_F64", 0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0) +
                  2 * pmc.get("SQ_INSTS_VALU_FMA_F64", 0)) * 64 * (lane or 1) / n
-        r["valu"] = {"issue_frac": issue / (SIMDS * CLOCK_HZ * avg_ms * 1e-3), "lane_utilisation": lane,
-                     "f64_tflops": flops / (avg_ms * 1e-3) / 1e12, "f64_peak_tflops": F64_PEAK_TFLOPS,
-                     "valu_insts_per_launch": pmc.get("SQ_INSTS_VALU", 0) / n}
+        r["valu"] = {"f64_flops_per_launch": flops, "f64_tflops": flops / sec / 1e12, "f64_peak_tflops": F64_PEAK_TFLOPS,
+                     "issue_frac": issue / (SIMDS * CLOCK_HZ * sec), "lane_utilisation": lane,
+                     "valu_insts_per_launch": pmc.get("SQ_INSTS_VALU", 0) / n,
+                     "note": "issue_frac: wave64 VALU issue cycles (f64 4, f32/int 2, transcendental 8/16) over "
+                             "1024 SIMDs x 2.4 GHz x launch time -- the resource that binds a cache-resident scene"}
         r["pmc_source"] = src
+    if bound == "hbm" and "algorithmic" in r:
+        r.update(unit="GB/s", peak=HBM_PEAK_GBS, achieved=r["algorithmic"]["GBs"], frac=r["algorithmic"]["frac_of_hbm"])
+    elif bound == "valu" and "valu" in r:
+        r.update(unit="TFLOP/s", peak=F64_PEAK_TFLOPS, achieved=r["valu"]["f64_tflops"],
+                 frac=r["valu"]["f64_tflops"] / F64_PEAK_TFLOPS)
     return r
 
 
@@ -145,15 +229,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="cornell_box_path", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=HEADLINE, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the frame's columns")
     ap.add_argument("--col-block", type=int, default=16)
     ap.add_argument("--no-events", action="store_true", help="A/B: time steps without per-launch HIP events")
     ap.add_argument("--spp", type=int, default=0, help="profiling only: override the config's spp (same launch "
                     "shapes, fewer batches); a bench line with it is not the config's number")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     rank, world, local = env_int("RANK", 0), env_int("WORLD_SIZE", 1), env_int("LOCAL_RANK", 0)
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -163,9 +253,9 @@ def main():
 
     import jsraytracer_amd as jr
     from jsraytracer_amd.tiles import FrameGather
-    from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline leg
+    from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline / parity legs
 
-    scene_name, W, H, spp, kind, depth = CONFIGS[args.config]
+    scene_name, W, H, spp, kind, depth, bound = CONFIGS[args.config]
     if args.spp > 0:
         spp = args.spp
     t_load = time.perf_counter()
@@ -186,14 +276,14 @@ def main():
     cb = args.col_block if world > 1 else 1
     fg = FrameGather(W, H, rank, world, cb, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
-
     STAGES = jr._native.STAGES
 
-    def step(events=None):
+    def step(events=None, colors=None):
         """events: None = no HIP events; 0 = every stage; else a bitmask of stages (jsrt.h stage_events)."""
-        st = scene.render_device(fg.local.data_ptr(), stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp,
-                                 max_depth=depth, kind=kind, seed=1, x_offset=rank if world > 1 else 0,
-                                 x_delt=world, stats=events is not None, stage_events=events or 0)
+        st = scene.render_device(fg.local.data_ptr(), colors.data_ptr() if colors is not None else None,
+                                 stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp, max_depth=depth,
+                                 kind=kind, seed=1, x_offset=rank if world > 1 else 0, x_delt=world,
+                                 stats=events is not None, stage_events=events or 0)
         fg.gather()
         return st
 
@@ -221,39 +311,65 @@ def main():
         stats = [step(1 << STAGES.index(dom))]
     dom_ms = sum(s["stage_ms"][dom] for s in stats) / len(stats)
     dom_launches = stats[0]["stage_launches"][dom]
-    # per-stage split: one more step after the timed region with every launch bracketed
-    st_after = step(0)
+    # per-stage split: one more step after the timed region with every launch bracketed; at N = 1 it
+    # also returns the f32 colours for the parity check (the same frame: the render is deterministic)
+    colors = torch.empty(fg.maxcols * H * 4, dtype=torch.float32, device=f"cuda:{local}") if world == 1 else None
+    st_after = step(0, colors)
     stage_ms, stage_launches, kernel_ms = st_after["stage_ms"], st_after["stage_launches"], st_after["kernel_ms"]
+    torch.cuda.synchronize()
 
+    par = None
     if rank == 0:
         total = W * H * spp
         value = total * args.steps / elapsed
-        cpu, counts = (None, None)
+        cpu, counts, ref = None, None, None
         if not args.no_cpu_baseline and world == 1:
-            cpu, counts = cpu_baseline(blob, W, H, spp, kind, depth)
-        roof = roofline(args.config, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp)
+            cpu, counts, ref = cpu_baseline(blob, W, H, spp, kind, depth)
+            js, js_sample = REFERENCE_JS.get(scene_name, (None, None))
+            if js:
+                cpu["reference_js"] = {"value": js, "unit": "pixel-samples/s", "cores": 8, "kind": "reference",
+                                       "sample": f"reference src/ under node 12, 8 worker_threads, {js_sample}; "
+                                                 "measured in the build container (BASELINE.md §2) -- the "
+                                                 "reference is absent on the GPU box"}
+        par = None
+        if not args.no_parity:
+            if ref is None:  # a few columns spread over the ranks' tiles (multi-GPU: checks the gather too)
+                threads = min(16, os.cpu_count() or 1)
+                dx = W // 4 + 17
+                ocol, orgba, _, _ = oracle_columns(blob, W, H, spp, kind, depth, 5, dx, threads)
+                ref = (ocol, orgba, 5, dx)
+            image = FrameGather.to_rgba8(fg.image)
+            cols = None
+            if colors is not None:  # world 1, col_block 1: owned column c is image column c
+                cols = colors.view(fg.maxcols, H, 4)[:W].permute(1, 0, 2).cpu().numpy()
+            par = parity(image, cols, ref)
+        roof = roofline(args.config, bound, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp)
+        size = f"{W}²" if W == H else f"{W}x{H}"
         line = {
-            "metric": "pixel-samples/sec + %HBM-roofline, cornell_box_path 1024² @1/2/4/8 GPU",
+            "metric": METRIC.format(scene=scene_name, size=size),
             "value": value, "unit": "pixel-samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64",
             "data": "reference scene graph (exported from the live reference, not synthetic), keyed RNG seed 1",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth} (Incremental)", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"tiles{world}",
-                       "col_block": cb},
-            "roofline": roof, "cpu_baseline": cpu,
+                       "col_block": cb, "headline": args.config == HEADLINE and args.spp == 0},
+            "roofline": roof, "cpu_baseline": cpu, "parity": par,
             "kernel_ms_per_step": kernel_ms,
             "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
             "events_lost": {"timed": sum(x["events_lost"] for x in stats), "stage_split": st_after["events_lost"]},
             "frame_attempts": [x["attempts"] for x in stats],
             "stages_note": "stage split from one fully-instrumented step after the timed region",
-            "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items()},
-            "stage_launches_per_step": stage_launches,
+            "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items() if v},
+            "stage_launches_per_step": {k: v for k, v in stage_launches.items() if v},
             "counts_per_sample": {k: round(v, 4) for k, v in counts.items() if k != "samples"} if counts else None,
         }
         print(json.dumps(line))
+        sys.stdout.flush()
     if world > 1:
         dist.destroy_process_group()
+    if par is not None and not par["pass"]:
+        print(f"bench: PARITY FAILURE against the oracle: {par}", file=sys.stderr)
 
 
 if __name__ == "__main__":

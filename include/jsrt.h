@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JSRT_ABI_VERSION 1
+#define JSRT_ABI_VERSION 2
 
 typedef struct jsrt_scene jsrt_scene;
 
@@ -48,14 +48,15 @@ typedef struct {
     int32_t reserved[4];
 } jsrt_params;
 
-#define JSRT_STAGES 8
+#define JSRT_STAGES 12
 typedef struct {
     double kernel_ms;        /* sum of all render-kernel durations (HIP events on the render stream) */
     double total_ms;         /* host wall time of the call */
     uint64_t samples;        /* pixel-samples rendered */
     uint32_t launches;       /* render-kernel launches */
     uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
-    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final, resolve */
+    double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final,
+                                            resolve, trace (extend+shade+shadow fused), 3 spare */
     uint32_t stage_launches[JSRT_STAGES];
     uint32_t attempts;       /* frame attempts: > 1 when a pool / launch bound was outgrown and the frame redone */
     uint32_t events_lost;    /* event pairs whose elapsed time HIP could not report (not in stage_ms) */

@@ -23,19 +23,21 @@ class Params(ctypes.Structure):
                 ("max_paths", ctypes.c_int32), ("stage_events", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
-STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve"]
+STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve", "k_trace",
+          "spare9", "spare10", "spare11"]
+NSTAGES = len(STAGES)  # JSRT_STAGES
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("samples", ctypes.c_uint64),
-                ("launches", ctypes.c_uint32), ("batches", ctypes.c_uint32), ("stage_ms", ctypes.c_double * 8),
-                ("stage_launches", ctypes.c_uint32 * 8), ("attempts", ctypes.c_uint32), ("events_lost", ctypes.c_uint32)]
+                ("launches", ctypes.c_uint32), ("batches", ctypes.c_uint32), ("stage_ms", ctypes.c_double * NSTAGES),
+                ("stage_launches", ctypes.c_uint32 * NSTAGES), ("attempts", ctypes.c_uint32), ("events_lost", ctypes.c_uint32)]
 
     def as_dict(self):
         return {"kernel_ms": self.kernel_ms, "total_ms": self.total_ms, "samples": int(self.samples),
                 "launches": int(self.launches), "batches": int(self.batches),
-                "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(8)},
-                "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(8)},
+                "stage_ms": {STAGES[k]: self.stage_ms[k] for k in range(NSTAGES) if not STAGES[k].startswith("spare")},
+                "stage_launches": {STAGES[k]: int(self.stage_launches[k]) for k in range(NSTAGES) if not STAGES[k].startswith("spare")},
                 "attempts": int(self.attempts), "events_lost": int(self.events_lost)}
 
 

@@ -1,14 +1,20 @@
-"""Builds libjsrt.so in-tree with hipcc for gfx950 (no JIT caches: the .so travels to the GPU box)."""
+"""Builds libjsrt.so in-tree with hipcc for gfx950 (no JIT caches: the .so travels to the GPU box).
+
+The level kernels are compiled once per kernel profile (render_pf.hip with -DJSRT_PF=..., see
+csrc/render_levels.h) as separate objects, all objects in parallel.
+"""
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libjsrt.so")
-SOURCES = ["render.hip", "capi.cpp", "scene_load.cpp", "mesh_build.cpp"]
-HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "scene_load.h", "sdf_program.h"]
+PROFILES = {"analytic": 0, "mesh": 9, "sdf": 4, "all": 15}  # device_scene.h PF_ANALYTIC / PF_MESH / PF_SDF / PF_ALL
+HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "render_levels.h", "scene_load.h",
+           "sdf_program.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")
 
@@ -17,16 +23,15 @@ ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-function"]
 
-
 INCLUDE = os.path.join(HERE, "..", "include")
 PUBLIC = ["jsrt.h", "jsrt_scene.h", "jsrt_mesh.h"]
-# per-source dependencies (objects are rebuilt only when these change; render.hip dominates build time)
-DEPS = {
-    "render.hip": HEADERS + ["jsrt.h", "jsrt_scene.h"],
-    "capi.cpp": HEADERS + ["jsrt.h", "jsrt_scene.h"],
-    "scene_load.cpp": HEADERS + ["jsrt.h", "jsrt_scene.h"],
-    "mesh_build.cpp": ["jsrt_mesh.h", "jsrt_scene.h"],
-}
+# objects: (object stem, source, extra defines, dependencies); an object is rebuilt only when these change
+UNITS = [("render", "render.hip", [], HEADERS + ["jsrt.h", "jsrt_scene.h"])]
+UNITS += [(f"render_pf{pf}", "render_pf.hip", [f"-DJSRT_PF={pf}"], HEADERS + ["jsrt.h", "jsrt_scene.h"])
+          for pf in PROFILES.values()]
+UNITS += [("capi", "capi.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
+          ("scene_load", "scene_load.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
+          ("mesh_build", "mesh_build.cpp", [], ["jsrt_mesh.h", "jsrt_scene.h"])]
 OBJ_FLAGS = [f for f in FLAGS if f != "-shared"]
 
 
@@ -41,33 +46,50 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def _obj(src, tag, defines):
-    return os.path.join(OUT, f"{os.path.splitext(src)[0]}{tag}.o")
+def _obj(stem, tag=""):
+    return os.path.join(OUT, f"{stem}{tag}.o")
+
+
+def _deps(src, deps):
+    return [os.path.join(CSRC, src)] + [_path(d) for d in deps]
 
 
 def _stale():
-    return any(_newer(_obj(s, "", ()), [os.path.join(CSRC, s)] + [_path(d) for d in DEPS[s]]) for s in SOURCES) or \
-        any(_newer(LIB, [_obj(s, "", ())]) for s in SOURCES)
+    objs = [_obj(stem) for stem, _, _, _ in UNITS]
+    return any(_newer(_obj(stem), _deps(src, deps)) for stem, src, _, deps in UNITS) or _newer(LIB, objs)
 
 
-def build(force=False, verbose=False, variant=None, defines=()):
-    """variant: build _build/libjsrt_<variant>.so with extra -D defines (A/B experiments)."""
+def build(force=False, verbose=False, variant=None, defines=(), profiles=None):
+    """variant: build _build/libjsrt_<variant>.so with extra -D defines (A/B experiments).  profiles:
+    for a variant, the kernel profiles (PF numbers) recompiled with the defines; the other objects are
+    the default build's (fast A/B of one scene class)."""
     os.makedirs(OUT, exist_ok=True)
     lib = LIB if variant is None else os.path.join(OUT, f"libjsrt_{variant}.so")
     tag = "" if variant is None else f"_{variant}"
     if variant is None and not force and not _stale():
         return LIB
-    objs = []
-    for s in SOURCES:  # one object per source: an edit recompiles only what depends on it
-        o = _obj(s, tag, defines)
-        deps = [os.path.join(CSRC, s)] + [_path(d) for d in DEPS[s]]
-        if force or variant is not None or _newer(o, deps):
-            cmd = [HIPCC] + OBJ_FLAGS + list(defines) + ["-c", os.path.join(CSRC, s), "-o", o + ".tmp"]
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
-            subprocess.run(cmd, check=True)
-            os.replace(o + ".tmp", o)
+    if variant is not None:
+        build(verbose=verbose)  # the default objects a partial variant links against
+    jobs, objs = [], []
+    for stem, src, defs, deps in UNITS:
+        mine = variant is not None and (profiles is None or any(stem == f"render_pf{p}" for p in profiles))
+        o = _obj(stem, tag if mine else "")
         objs.append(o)
+        if force or mine or _newer(o, _deps(src, deps)):
+            cmd = [HIPCC] + OBJ_FLAGS + defs + (list(defines) if mine else []) + ["-c", os.path.join(CSRC, src),
+                                                                                 "-o", o + ".tmp"]
+            jobs.append((cmd, o))
+
+    def run(job):
+        cmd, o = job
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(o + ".tmp", o)
+
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(run, jobs))
     cmd = [HIPCC] + FLAGS + objs + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -79,4 +101,6 @@ def build(force=False, verbose=False, variant=None, defines=()):
 if __name__ == "__main__":
     args = sys.argv[1:]
     var = args[args.index("--variant") + 1] if "--variant" in args else None
-    print(build(force="--force" in args, verbose=True, variant=var, defines=[a for a in args if a.startswith("-D")]))
+    prof = [int(x) for x in args[args.index("--profiles") + 1].split(",")] if "--profiles" in args else None
+    print(build(force="--force" in args, verbose=True, variant=var, defines=[a for a in args if a.startswith("-D")],
+                profiles=prof))

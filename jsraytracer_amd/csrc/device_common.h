@@ -624,6 +624,26 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
     }
 }
 
+// Conservative cull of one top-level object: false only when the object provably
+// cannot produce an accepted hit on the segment (minD, flim): the ray misses its world box inflated
+// by k|o| + e0 (flim = (float) of the far limit min(best, maxD)).
+__device__ __forceinline__ bool root_needed(const RootBound &RB, F3 o, float ix, float iy, float iz, float oabs,
+                                            float fminD, float flim) {
+    if (!RB.bounded) return true;
+    const float e = RB.k * oabs + RB.e0;
+    float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
+    float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
+    a0 = (RB.lo[1] - e - o.y) * iy;
+    a1 = (RB.hi[1] + e - o.y) * iy;
+    tn = fmaxf(tn, fminf(a0, a1));
+    tf = fminf(tf, fmaxf(a0, a1));
+    a0 = (RB.lo[2] - e - o.z) * iz;
+    a1 = (RB.hi[2] + e - o.z) * iz;
+    tn = fmaxf(tn, fminf(a0, a1));
+    tf = fminf(tf, fmaxf(a0, a1));
+    return (tn <= tf) && (tf >= fminD) && (tn <= flim);
+}
+
 // World.cast (world.js:28-30); ANY = shadow query (only `0 < d < 1` of the closest is read,
 // materials.js:250-252, so the first accepted hit decides).
 //
@@ -649,22 +669,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     float flim = (float)maxD;  // (float)min(best, maxD): the cull's far limit, updated with best
     for (int i = 0; i < S.n_roots; ++i) {
         const DRoot &R = S.rootrec[i];
-        const RootBound &RB = R.rb;
-        bool need = live;
-        if (RB.bounded) {
-            const float e = RB.k * oabs + RB.e0;
-            float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
-            float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
-            a0 = (RB.lo[1] - e - o.y) * iy;
-            a1 = (RB.hi[1] + e - o.y) * iy;
-            tn = fmaxf(tn, fminf(a0, a1));
-            tf = fminf(tf, fmaxf(a0, a1));
-            a0 = (RB.lo[2] - e - o.z) * iz;
-            a1 = (RB.hi[2] + e - o.z) * iz;
-            tn = fmaxf(tn, fminf(a0, a1));
-            tf = fminf(tf, fmaxf(a0, a1));
-            need = need && (tn <= tf) && (tf >= fminD) && (tn <= flim);
-        }
+        const bool need = live && root_needed(R.rb, o, ix, iy, iz, oabs, fminD, flim);
         if (!__any(need)) continue;
 #ifdef JSRT_DBG_COUNT
         {
@@ -722,24 +727,6 @@ struct MarchState {
     int steps, g, prim;
     bool marching;
 };
-
-// The conservative world-box cull of world_cast for one top-level object.
-__device__ __forceinline__ bool root_needed(const RootBound &RB, F3 o, float ix, float iy, float iz, float oabs,
-                                            float fminD, float flim) {
-    if (!RB.bounded) return true;
-    const float e = RB.k * oabs + RB.e0;
-    float a0 = (RB.lo[0] - e - o.x) * ix, a1 = (RB.hi[0] + e - o.x) * ix;
-    float tn = fminf(a0, a1), tf = fmaxf(a0, a1);
-    a0 = (RB.lo[1] - e - o.y) * iy;
-    a1 = (RB.hi[1] + e - o.y) * iy;
-    tn = fmaxf(tn, fminf(a0, a1));
-    tf = fminf(tf, fmaxf(a0, a1));
-    a0 = (RB.lo[2] - e - o.z) * iz;
-    a1 = (RB.hi[2] + e - o.z) * iz;
-    tn = fmaxf(tn, fminf(a0, a1));
-    tf = fminf(tf, fmaxf(a0, a1));
-    return (tn <= tf) && (tf >= fminD) && (tn <= flim);
-}
 
 // Advance a lane's cast through the top-level objects until it must march an SDF primitive
 // (returns with m.marching) or the cast is complete (m.root == n_roots).

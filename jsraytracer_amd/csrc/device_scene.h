@@ -47,7 +47,7 @@ struct DInst {           // one node of the object tree flattened per path (shar
     int32_t pad[2];
 };
 
-struct RootBound {       // conservative world-space box of one top-level object (culling only)
+struct RootBound {       // conservative world-space bound of one top-level object (culling only)
     float lo[3];
     float k;             // margin per unit of |ray origin|_inf
     float hi[3];

@@ -17,407 +17,15 @@
 //   k_final    running mean + PixelBuffer.setColor rules -> RGBA8 (+ f32 colour)
 // Every kernel is small and converged (all lanes run the same stage) with its own register
 // budget; batches are (pixels x samples) with ray SoA buffers in HBM.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <stdlib.h>
-#include <string.h>
+#include "render_levels.h"
 
-#include <algorithm>
-#include <vector>
-
-#include "device_common.h"
-#include "render_kernel.h"
-
-#ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade (register budget)
-#define JSRT_SHADE_OCC 2
-#endif
-// k_shadow / k_extend: at least 6 / 5 waves per SIMD.  Their casts are latency-bound (BVH node and
-// scene loads on a dependent chain), so more resident waves beat the registers the compiler would
-// otherwise keep (A/B on MI355X: cornell +3 %, bunny +15 %, dragon +4 % against no bound; 8 waves
-// for k_shadow spills and loses 11 % on cornell).
-#ifndef JSRT_SHADOW_OCC
-#define JSRT_SHADOW_OCC 6
-#endif
-#ifndef JSRT_EXTEND_OCC
-#define JSRT_EXTEND_OCC 5
-#endif
-// optional waves-per-EU window (min, max) per kernel for A/B occupancy experiments
-#ifdef JSRT_SHADOW_WPE
-#define SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(JSRT_SHADOW_WPE)))
-#else
-#define SHADOW_ATTR
-#endif
-#ifdef JSRT_SHADE_WPE
-#define SHADE_ATTR __attribute__((amdgpu_waves_per_eu(JSRT_SHADE_WPE)))
-#else
-#define SHADE_ATTR
-#endif
+#include <mutex>
 
 namespace jsrt {
 
 const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final",
-                                    "k_resolve"};
-constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;  // camera ray: its result is the path's root colour
-constexpr uint32_t DEAD_RAY = 0xFFFFFFFEu;   // level-0 slot of a path outside the image (no result)
-constexpr int32_t NO_RAY = -2;                // W.prim of a slot that holds no ray to trace
+                                    "k_resolve", "k_trace"};
 
-// block-aggregated append (one atomic per block: same-address atomics serialise device-wide).
-// Every thread of the block must call it.
-template <int NT>
-__device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
-    constexpr int NW = NT / 64;
-    __shared__ uint32_t s_off[NW + 1];
-    const uint64_t b1 = __ballot(n >= 1), b2 = __ballot(n >= 2);
-    const int lane = (int)__lane_id(), wid = (int)(threadIdx.x >> 6);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t pre = (uint32_t)(__popcll(b1 & lt) + __popcll(b2 & lt));
-    if (lane == 0) s_off[wid] = (uint32_t)(__popcll(b1) + __popcll(b2));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t c = s_off[w];
-            s_off[w] = acc;
-            acc += c;
-        }
-        s_off[NW] = acc ? atomicAdd(counter, acc) : 0u;
-    }
-    __syncthreads();
-    return s_off[NW] + s_off[wid] + pre;
-}
-
-__device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
-    const uint32_t p = W.parent[i];
-    if (p == DEAD_RAY) return;
-    if (p == NO_PARENT) {
-        float *dst = W.root + 3 * (size_t)W.path[i];
-        dst[0] = c.x;
-        dst[1] = c.y;
-        dst[2] = c.z;
-    } else {
-        W.slot[(size_t)(p & 1u) * W.nstride + (p >> 1)] = make_float4(c.x, c.y, c.z, 0.0f);
-    }
-}
-
-// patch-ordered owned pixel index -> (owned column c, row py, image column px)
-__device__ __forceinline__ bool pixel_of(const RenderArgs &A, uint32_t p, int &c, int &py, int &px) {
-    const int patch = (int)(p >> 6), lane = (int)(p & 63);
-    c = (patch % A.patches_x) * 8 + (lane & 7);
-    py = (patch / A.patches_x) * 8 + (lane >> 3);
-    if (c >= A.ncols || py >= A.H) return false;
-    px = owned_to_px(c, A.x_offset, A.x_delt, A.col_block);
-    return px < A.W;
-}
-
-__device__ __forceinline__ F3 pick(bool f, F3 a, F3 b) { return f3(f ? a.x : b.x, f ? a.y : b.y, f ? a.z : b.z); }
-__device__ __forceinline__ Child pick(bool f, const Child &a, const Child &b) {
-    return Child{pick(f, a.dir, b.dir), pick(f, a.col, b.col), pick(f, a.w, b.w), f ? a.k : b.k};
-}
-
-// Tree schedule: level L of the batch occupies pool slots [base, base + count).  Counts live on
-// the device (k_gen writes level 0, k_shade appends level L + 1), so the host enqueues every level
-// without reading them back; an overflowed batch reads as empty everywhere and is redone.
-struct LevelRange {
-    uint32_t base, count;
-};
-__device__ __forceinline__ LevelRange level_range(const WArgs &W, int L) {
-    if (W.lvl[LVL_FLAG]) return LevelRange{0u, 0u};
-    uint32_t b = 0;
-    for (int j = 0; j < L; ++j) b += W.lvl[j];
-    return LevelRange{b, W.lvl[L]};
-}
-
-// The material data k_shade hands to k_shadow for one lit node (after getBaseFactors), plus the
-// node's RNG frame (its light-sample draws come first, materials.js:244-257).
-struct Handoff {
-    F3 pos, N, R, refr, diff, spec;
-    double kr, smoothness;
-    int32_t mkind;
-    uint32_t addr, key;
-};
-struct NodeOut {
-    F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
-    uint32_t info;  // INFO_* bits + child count
-    Handoff h;      // h.pos (the hit point) is set for every hit; the rest for lit nodes
-};
-
-// World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
-// Geometry.materialData + Material.color (materials.js).  Fills the node (info, ambient / surface,
-// shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
-template <int PF>
-__device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
-                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1) {
-    const DPrim &P = S.prims[h.prim];
-    // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409); the host
-    // precomputed it (same operations) for identity prims and for the top-level context
-    double inv[16];
-    {
-        const int ps = S.prim_shade[h.prim];
-        if (ps < 0 || h.ctx == 0) {
-            const double *src = ps < 0 ? S.shadeI + 16 * h.ctx : S.shade0 + 16 * ps;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) inv[k] = src[k];
-        } else {
-            const double *C = S.ctx + 16 * h.ctx;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const double a0 = r < 3 ? P.inv[4 * r + 0] : 0.0, a1 = r < 3 ? P.inv[4 * r + 1] : 0.0,
-                                 a2 = r < 3 ? P.inv[4 * r + 2] : 0.0, a3 = r < 3 ? P.inv[4 * r + 3] : 1.0;
-                    double s = 0;
-                    s += a0 * C[c];
-                    s += a1 * C[4 + c];
-                    s += a2 * C[8 + c];
-                    s += a3 * C[12 + c];
-                    inv[4 * r + c] = s;
-                }
-        }
-    }
-    const bool need_uv = (S.mat_flags[P.material] & MATF_UV) != 0;
-    const F3 lo = xf_point(inv, o), ld = xf_dir(inv, d);
-    const F3 pl = ray_point(lo, ld, h.t);  // base_data.position (local)
-    F3 nrm = f3(0, 0, 0);
-    float nrm_w = 0.0f;
-    float u = 0, v = 0;
-    F3 basecolor = f3(1, 1, 1);
-    switch (P.gkind) {
-    case JSRT_GEOM_PLANE:
-    case JSRT_GEOM_SQUARE:
-    case JSRT_GEOM_CIRCLE:  // SimplePlane.materialData (geometry.js:249-254)
-        nrm = f3(0, 0, 1);
-        u = pl.x;
-        v = pl.y;
-        break;
-    case JSRT_GEOM_SPHERE: {  // geometry.js:449-455: position.normalized() includes w = 1
-        const double nn = sqrt(dot3(pl, pl) + 1.0);
-        nrm = pl;
-        nrm_w = 1.0f;
-        if (nn > 0.00001) { nrm = scale(pl, 1 / nn); nrm_w = (float)(1.0 * (1 / nn)); }
-        if (need_uv) cart_to_sph(nrm, u, v);
-        break;
-    }
-    case JSRT_GEOM_CYLINDER:  // geometry.js:479-487
-        nrm = normalized(f3(pl.x, pl.y, 0));
-        if (need_uv) {
-            u = (float)(0.5 + atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
-            v = (float)(0.5 + (double)pl.z);
-        }
-        break;
-    case JSRT_GEOM_AABB: {  // geometry.js:210-224
-        double norm_dist = 0;
-        const float pc[3] = {pl.x, pl.y, pl.z};
-        float nn[3] = {0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const double comp = ((double)pc[i] - (double)P.center[i]) / (double)P.half[i];
-            const double ac = fabs(comp);
-            if (ac > norm_dist) {
-                norm_dist = ac;
-                nn[0] = nn[1] = nn[2] = 0;
-                nn[i] = (float)js_sign(comp);
-            }
-        }
-        nrm = f3(nn[0], nn[1], nn[2]);
-        break;
-    }
-    case JSRT_GEOM_TRIANGLE: {  // geometry.js:376-409
-        if (!(PF & PF_TRI)) break;
-        const DTri &T = S.tris[P.gindex];
-        nrm = f3(T.n[0], T.n[1], T.n[2]);
-        if (T.shade >= 0) {
-            const DTriShade &TS = S.trish[T.shade];
-            const F3 v2 = f3(pl.x - T.p0[0], pl.y - T.p0[1], pl.z - T.p0[2]);
-            const double d20 = dot3(v2, f3(T.v0[0], T.v0[1], T.v0[2])), d21 = dot3(v2, f3(T.v1[0], T.v1[1], T.v1[2]));
-            const double bv = (T.d11 * d20 - T.d01 * d21) / T.denom, bw = (T.d00 * d21 - T.d01 * d20) / T.denom;
-            const float b0 = (float)(1 - bv - bw), b1 = (float)bv, b2 = (float)bw;
-            if (TS.has_uv) {
-                u = (TS.uv[0][0] * b0 + TS.uv[1][0] * b1) + TS.uv[2][0] * b2;
-                v = (TS.uv[0][1] * b0 + TS.uv[1][1] * b1) + TS.uv[2][1] * b2;
-            }
-            if (TS.has_normal) {
-                nrm = f3((TS.vn[0][0] * b0 + TS.vn[1][0] * b1) + TS.vn[2][0] * b2,
-                         (TS.vn[0][1] * b0 + TS.vn[1][1] * b1) + TS.vn[2][1] * b2,
-                         (TS.vn[0][2] * b0 + TS.vn[1][2] * b1) + TS.vn[2][2] * b2);
-                nrm_w = (TS.vn[0][3] * b0 + TS.vn[1][3] * b1) + TS.vn[2][3] * b2;
-            }
-        }
-        break;
-    }
-    case JSRT_GEOM_SDF: {  // SDFGeometry.materialData (sdf.js:41-47)
-        if (!(PF & PF_SDF)) break;
-        const jsrt_rec_sdfgeom &G = S.sdfg[P.gindex];
-        const double dist0 = sdf_node_dist(S, G.root, pl);
-        const float step = (float)G.normal_step;
-        const float nx = (float)((sdf_node_dist(S, G.root, f3(pl.x + step, pl.y + 0.0f, pl.z + 0.0f)) - dist0) / G.normal_step);
-        const float ny = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + step, pl.z + 0.0f)) - dist0) / G.normal_step);
-        const float nz = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + 0.0f, pl.z + step)) - dist0) / G.normal_step);
-        const SdfMD md = sdf_material(S, G.root, pl);
-        if (md.has_bc) basecolor = md.bc;
-        if (md.has_uv) { u = md.u; v = md.v; }
-        nrm = normalized(f3(nx, ny, nz));
-        break;
-    }
-    default: break;
-    }
-    // normal = inv_transform.transposed().times(normal).to4(0).normalized()  (world.js:133-134)
-    F3 N;
-    {
-        const float wx = (float)((((double)nrm.x * inv[0] + (double)nrm.y * inv[4]) + (double)nrm.z * inv[8]) + (double)nrm_w * inv[12]);
-        const float wy = (float)((((double)nrm.x * inv[1] + (double)nrm.y * inv[5]) + (double)nrm.z * inv[9]) + (double)nrm_w * inv[13]);
-        const float wz = (float)((((double)nrm.x * inv[2] + (double)nrm.y * inv[6]) + (double)nrm.z * inv[10]) + (double)nrm_w * inv[14]);
-        N = normalized(f3(wx, or0(wy), or0(wz)));
-    }
-    ShadeData sd;
-    sd.pos = ray_point(o, d, h.t);  // material_data.position = ray.getPoint(distance)
-    out.h.pos = sd.pos;
-    out.h.addr = addr;
-    out.h.key = key;
-    const jsrt_rec_material &M = S.mat[P.material];
-    const int mkind = (int)M.kind;
-    Rng rng{key, addr, 0};
-    if (mkind == JSRT_MAT_SOLID) {
-        out.surf = mc_eval(S, M.color, u, v);
-        out.info = INFO_HIT;
-        return 0;
-    }
-    if (mkind == JSRT_MAT_TRANSPARENT) {  // materials.js:169-173
-        out.surf = scale(mc_eval(S, M.color, u, v), M.opacity);
-        ch0 = Child{d, f3(1, 1, 1), f3(1, 1, 1), 1 - M.opacity};
-        out.info = INFO_HIT | (1u << INFO_NCHILD_SHIFT);
-        return 1;
-    }
-    // getBaseFactors (materials.js:210-238)
-    sd.V = neg(normalized(d));
-    F3 Nn = normalized(N);
-    sd.backside = false;
-    double vdotn = dot3(sd.V, Nn);
-    if (vdotn < 0) {
-        Nn = neg(Nn);
-        sd.backside = true;
-        vdotn = -vdotn;
-    }
-    sd.N = Nn;
-    sd.vdotn = vdotn;
-    sd.R = normalized(sub(scale(Nn, 2 * vdotn), sd.V));
-    sd.ambient = mul(basecolor, mc_eval(S, M.ambient, u, v));
-    sd.diff = mul(basecolor, mc_eval(S, M.diffuse, u, v));
-    sd.spec = mc_eval(S, M.specular, u, v);
-    sd.refl = mc_eval(S, M.reflect, u, v);
-    sd.trans = mc_eval(S, M.transmit, u, v);
-    sd.smoothness = M.smoothness;
-    sd.kr = 1;
-    sd.has_refr = false;
-    sd.refr = f3(0, 0, 0);
-    if (mkind != JSRT_MAT_PHONG) {
-        const double ratio = M.ratio;
-        // fresnelReflectionFactor (materials.js:366-386)
-        double kr;
-        if (!__builtin_isfinite(ratio)) kr = 1;
-        else {
-            const double ni = sd.backside ? ratio : 1, nt = sd.backside ? 1 : ratio;
-            const double cosi = vdotn, sint = ni / nt * sqrt(js_max(0, 1 - cosi * cosi));
-            if (sint >= 1) kr = 1;
-            else {
-                const double cost = sqrt(js_max(0, 1 - sint * sint));
-                const double Rs = ((nt * cosi) - (ni * cost)) / ((nt * cosi) + (ni * cost));
-                const double Rp = ((ni * cosi) - (nt * cost)) / ((ni * cosi) + (nt * cost));
-                kr = (Rs * Rs + Rp * Rp) / 2;
-            }
-        }
-        sd.kr = kr;
-        // getRefractionDirection (materials.js:358-364)
-        const double r = sd.backside ? ratio : 1 / ratio, k = 1 - r * r * (1 - vdotn * vdotn);
-        if (!(k < 0)) {
-            sd.has_refr = true;
-            sd.refr = add(scale(neg(sd.V), r), scale(Nn, r * vdotn - sqrt(k)));
-        }
-    }
-    // colorFromLights (materials.js:240-259): k_shadow evaluates the light samples (one lane each,
-    // RNG calls [0, light_draws) of this frame) from the material data handed off here; the
-    // scatter draws below follow them (calls light_draws, ...)
-    out.surf = sd.ambient;
-    uint32_t info = INFO_HIT;
-    if (lit) {
-        info |= INFO_LIT;
-        out.h.N = sd.N;
-        out.h.R = sd.R;
-        out.h.refr = sd.refr;
-        out.h.diff = sd.diff;
-        out.h.spec = sd.spec;
-        out.h.kr = sd.kr;
-        out.h.mkind = mkind;
-        out.h.smoothness = M.smoothness;
-        rng.calls = (uint32_t)S.light_draws;
-    }
-    int n = 0;
-    auto push = [&](const Child &c) {  // unconditional selects keep both slots in registers
-        const bool first = n == 0;
-        ch0 = pick(first, c, ch0);
-        ch1 = pick(first, ch1, c);
-        ++n;
-    };
-    if (mkind == JSRT_MAT_PHONG) {  // materials.js:277-288
-        if (dot3(sd.refl, sd.refl) > 0) push(Child{sd.R, f3(1, 1, 1), sd.refl, 1.0});
-        if (dot3(sd.trans, sd.trans) > 0) push(Child{normalized(d), f3(1, 1, 1), sd.trans, 1.0});
-    } else {  // materials.js:315-330
-        if (sd.kr > 0) {
-            F3 dir = sd.R, col = f3(1, 1, 1);
-            bool ok = true;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col);
-            if (ok) push(Child{dir, col, sd.refl, sd.kr});
-        }
-        if (sd.kr < 1) {
-            F3 dir = sd.refr, col = f3(1, 1, 1);
-            bool ok = sd.has_refr;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col);
-            if (ok) push(Child{dir, col, sd.trans, 1 - sd.kr});
-        }
-    }
-    out.info = info | ((uint32_t)n << INFO_NCHILD_SHIFT);
-    return n;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Node / hand-off storage (AoS float4 records: one or two 16-B accesses per lane)
-__device__ __forceinline__ float u2f(uint32_t x) { return __uint_as_float(x); }
-__device__ __forceinline__ uint32_t f2u(float x) { return __float_as_uint(x); }
-
-__device__ __forceinline__ void store_node(const WArgs &W, uint32_t i, F3 c, uint32_t info) {
-    W.node[i] = make_float4(c.x, c.y, c.z, u2f(info));
-}
-__device__ __forceinline__ void store_child(const WArgs &W, uint32_t i, uint32_t j, const Child &c) {
-    float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
-    x[0] = make_float4(c.col.x, c.col.y, c.col.z, c.w.x);
-    x[W.nstride] = make_float4(c.w.y, c.w.z, u2f((uint32_t)__double2loint(c.k)), u2f((uint32_t)__double2hiint(c.k)));
-}
-// ((v * col) * w) * k added to c: surface.plus(child.times(col).times(w).times(k)) (materials.js:277-330)
-__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v) {
-    const float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
-    const float4 a = x[0], b = x[W.nstride];
-    const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
-    return add(c, scale(mul(mul(v, f3(a.x, a.y, a.z)), f3(a.w, b.x, b.y)), k));
-}
-__device__ __forceinline__ void store_hand(const WArgs &W, uint32_t h, const Handoff &o) {
-    float4 *p = W.hand + h;
-    const size_t hs = W.hstride;
-    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f((uint32_t)o.mkind));
-    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f((uint32_t)__double2loint(o.kr)));
-    p[2 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f((uint32_t)__double2hiint(o.kr)));
-    p[3 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f(o.addr));
-    p[4 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(o.key));
-    p[5 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2loint(o.smoothness)));
-    p[6 * hs] = make_float4(u2f((uint32_t)__double2hiint(o.smoothness)), 0.0f, 0.0f, 0.0f);
-}
-
-// per pixel, the renderer's f32 accumulation of one sample (renderers.js:93-97, 52-61)
-__device__ __forceinline__ F3 accumulate(const RenderArgs &A, F3 acc, F3 col) {
-    if (A.kind == JSRT_RENDERER_RANDOM) return add(acc, scale(col, 1.0 / A.spp));
-    if (A.kind == JSRT_RENDERER_INCREMENTAL) return f3(acc.x + col.x, acc.y + or0(col.y), acc.z + or0(col.z));  // buffer.plus(c.to4(true))
-    return col;
-}
-
-// ---------------------------------------------------------------------------------------------
 // camera rays: one per path q of the batch, sample-major (neighbouring q are neighbouring pixels)
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;
@@ -456,323 +64,6 @@ __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     W.addr[q] = mix32(0u, 1u);
     W.key[q] = key;
     W.prim[q] = -1;
-}
-
-// Closest hit (World.cast, world.js:28-30).  Chain: ray q of the batch; tree: level L's range.
-template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L, double minD) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    uint32_t i = t;
-    if (CHAIN) {
-        if (t >= W.npaths) return;
-    } else {
-        const LevelRange R = level_range(W, L);
-        if (t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // the launch bound was too small
-        if (t >= R.count) return;
-        i = R.base + t;
-    }
-    if (W.prim[i] == NO_RAY) return;
-    const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
-    const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
-    W.t[i] = h.t;
-    W.prim[i] = h.prim;
-    W.ctx[i] = h.ctx;
-}
-
-// World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
-// Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
-// Tree schedule: node = pool slot; children are appended to level L + 1 (block-aggregated).
-template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene S, WArgs W, int L, int child_depth) {
-    const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
-    uint32_t count = W.npaths, base = 0, next_base = 0;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-        next_base = R.base + R.count;
-        if (t0 >= count) return;  // block-uniform: every thread of a live block reaches block_append
-    } else if (tt >= count) {
-        return;
-    }
-    const bool in = tt < count;
-    const uint32_t q = in ? tt : 0u;                                     // ray slot (chain) / level index (tree)
-    const uint32_t i = CHAIN ? (uint32_t)L * W.npaths + q : base + q;    // node index
-    const uint32_t r = CHAIN ? q : i;                                    // ray index
-    int nchild = 0;
-    Child ch0, ch1;
-    NodeOut out;
-    bool hit = false;
-    const int prim = in ? W.prim[r] : NO_RAY;
-    if (prim == NO_RAY) {
-        if (in) store_node(W, i, f3(0, 0, 0), 0u);
-    } else if (prim < 0) {  // miss: World.color returns bg_color (world.js:35-36)
-        const F3 bg = f3(S.bg[0], S.bg[1], S.bg[2]);
-        if (CHAIN) {
-            store_node(W, i, bg, INFO_MISS);
-            W.prim[r] = NO_RAY;
-        } else {
-            write_result(W, i, bg);
-            store_node(W, i, bg, 0u);
-        }
-    } else {
-        hit = true;
-        const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
-        const Hit h{W.t[r], prim, W.ctx[r]};
-        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
-        store_node(W, i, out.surf, out.info);
-        if (out.info & INFO_LIT) store_hand(W, q, out.h);
-        if (nchild > 0) store_child(W, i, 0, ch0);
-        if (nchild > 1) store_child(W, i, 1, ch1);
-    }
-    if (CHAIN) {  // the child ray (World.color(child, depth - 1)) takes over slot q
-        if (!hit) return;
-        if (child_depth > 0 && nchild > 0) {
-            W.ox[r] = out.h.pos.x; W.oy[r] = out.h.pos.y; W.oz[r] = out.h.pos.z;
-            W.dx[r] = ch0.dir.x; W.dy[r] = ch0.dir.y; W.dz[r] = ch0.dir.z;
-            W.addr[r] = mix32(out.h.addr, 1u);
-        } else {
-            W.prim[r] = NO_RAY;  // no child, or children black without a cast (depth 0)
-        }
-        return;
-    }
-    // tree: children append to level L + 1; at depth 0 they are black without a cast
-    const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
-    if (!hit || nchild == 0) return;
-    if (child_depth == 0) {
-        W.slot[i] = make_float4(0, 0, 0, 0);
-        if (nchild > 1) W.slot[W.nstride + i] = make_float4(0, 0, 0, 0);
-        return;
-    }
-    if ((size_t)at + nchild > W.level_cap || (size_t)next_base + at + nchild > W.pool) {
-        W.lvl[LVL_FLAG] = 1u;  // outgrew the pool: the host redoes the frame with a larger one
-        return;
-    }
-    const uint32_t path = W.path[r];
-    for (int j = 0; j < nchild; ++j) {
-        const Child &c = j == 0 ? ch0 : ch1;
-        const uint32_t rr = next_base + at + (uint32_t)j;
-        W.ox[rr] = out.h.pos.x; W.oy[rr] = out.h.pos.y; W.oz[rr] = out.h.pos.z;
-        W.dx[rr] = c.dir.x; W.dy[rr] = c.dir.y; W.dz[rr] = c.dir.z;
-        W.addr[rr] = mix32(out.h.addr, (uint32_t)j + 1);
-        W.key[rr] = out.h.key;
-        W.path[rr] = path;
-        W.parent[rr] = 2 * i + (uint32_t)j;
-        W.prim[rr] = -1;
-    }
-}
-
-// The light samples of the lit nodes of level L (lights.js sampleIterator), their shadow casts
-// (materials.js:250-252), colorFromLightSample (materials.js:261-269, 340-356) and the
-// colorFromLights sums (materials.js:244-257), which turn the node's ambient into its surface.
-// W.group lanes serve one node (sample s on lane s, a power of two >= ns); the node's first lane
-// adds the samples in the reference's order from its neighbours' registers.  SERIAL (more than 64
-// samples per node, group 1): one lane per node walks all samples itself.
-// One light sample of a lit node without its shadow cast: the light sample (lights.js), its
-// unshadowed colour (colorFromLightSample) and the shadow ray (origin P = the hit point, direction
-// delta, accepted distances (1e-4, 1), materials.js:250-252).
-template <int PF>
-__device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
-    const float4 h0 = hp[0];
-    P = f3(h0.x, h0.y, h0.z);
-    Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
-    F3 L, lcol;
-    light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
-    const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
-    ShadeData sd;
-    sd.N = f3(h1.x, h1.y, h1.z);
-    sd.R = f3(h2.x, h2.y, h2.z);
-    sd.refr = f3(h3.x, h3.y, h3.z);
-    sd.diff = f3(h4.x, h4.y, h4.z);
-    sd.spec = f3(h5.x, h5.y, h5.z);
-    sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
-    sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
-#ifdef JSRT_AB_NOCOLOR
-    return lcol;
-#else
-    return light_sample_color((int)f2u(h0.w), sd, L, lcol);
-#endif
-}
-
-__device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
-
-template <int PF>
-__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s) {
-    F3 P, delta;
-    const F3 c = sample_unshadowed<PF>(S, hp, hs, s, P, delta);
-    // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
-    // (the light behind the surface, a black material, an edge-on area light) adds the same
-    // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
-    if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return f3(0, 0, 0);
-#ifdef JSRT_AB_NOCAST
-    const Hit sh{DINF, -1, 0};
-#else
-    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
-#endif
-    if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
-    return c;
-}
-
-// colorFromLights: per light, its samples in order (a shadowed sample adds +0, which never changes
-// an f32 running sum that starts at +0), times 1/samples, added to the ambient `ret`.  Sample s of
-// the node sits on lane (lane & ~(G - 1)) + s; every lane takes part in the shuffles.
-__device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3 c) {
-    const int lane0 = (int)(__lane_id() & ~(G - 1));
-    uint32_t k = 0;
-    for (int li = 0; li < S.n_lights; ++li) {
-        const DLight &Lt = S.lights[li];
-        const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
-        F3 light_color = f3(0, 0, 0);
-        for (int j = 0; j < n; ++j, ++k) {
-            const int src = lane0 + (int)k;
-            light_color = add(light_color, f3(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src)));
-        }
-        if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
-    }
-    return ret;
-}
-
-template <int PF, bool CHAIN, bool SERIAL>
-__global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
-    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t q = e / G, s = e % G;  // G is a power of two
-    const bool in = q < count;
-    const uint32_t i = base + (in ? q : 0u);
-    const float4 nd = W.node[i];
-    const bool lit = in && (f2u(nd.w) & INFO_LIT);
-    const float4 *hp = W.hand + (in ? q : 0u);
-    F3 ret = f3(nd.x, nd.y, nd.z);  // ambient
-    if (SERIAL) {  // one lane per node: every sample in order
-        if (!lit) return;
-        uint32_t k = 0;
-        for (int li = 0; li < S.n_lights; ++li) {
-            const DLight &Lt = S.lights[li];
-            const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
-            F3 light_color = f3(0, 0, 0);
-            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k));
-            if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
-        }
-        W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
-        return;
-    }
-    F3 c = f3(0, 0, 0);
-    if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s);
-    ret = light_sums(S, G, ret, c);
-    if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Persistent casts for SDF scenes (device_common.h persistent_cast): same results as k_extend /
-// k_shadow, with lanes refilled from a work counter while other lanes keep marching.
-struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
-    const WArgs &W;
-    uint32_t base;
-    __device__ __forceinline__ bool load(uint32_t j, F3 &o, F3 &d) const {
-        const uint32_t i = base + j;
-        if (W.prim[i] == NO_RAY) return false;
-        o = f3(W.ox[i], W.oy[i], W.oz[i]);
-        d = f3(W.dx[i], W.dy[i], W.dz[i]);
-        return true;
-    }
-    __device__ __forceinline__ void store(uint32_t j, const Hit &h) const {
-        const uint32_t i = base + j;
-        W.t[i] = h.t;
-        W.prim[i] = h.prim;
-        W.ctx[i] = h.ctx;
-    }
-};
-
-template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256) void k_extend_q(DScene S, WArgs W, int L, double minD) {
-    uint32_t count = W.npaths, base = 0;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
-    ExtendSrc src{W, base};
-    persistent_cast<PF, false>(S, W.qctr + L, count, minD, DINF, true, src);
-}
-
-struct ShadowSrc {  // the light samples' shadow rays written by k_shadow_prep
-    const WArgs &W;
-    __device__ __forceinline__ bool load(uint32_t e, F3 &o, F3 &d) const {
-        const float4 c = W.scol[e];
-        if (f2u(c.w) != 1u) return false;
-        const float4 a = W.sray[e], b = W.sray[W.sstride + e];
-        o = f3(a.x, a.y, a.z);
-        d = f3(b.x, b.y, b.z);
-        return true;
-    }
-    __device__ __forceinline__ void store(uint32_t e, const Hit &h) const {
-        if (shadowed(h)) W.scol[e].w = u2f(2u);
-    }
-};
-
-// k_shadow's lane layout (node q on lanes [q * G, q * G + G), sample s on lane s): the unshadowed
-// colour and shadow ray of every light sample
-template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
-    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t q = e / G, s = e % G;
-    if (q >= count || s >= ns) return;
-    const float4 nd = W.node[base + q];
-    if (!(f2u(nd.w) & INFO_LIT)) return;
-    F3 P, delta;
-    const F3 c = sample_unshadowed<PF>(S, W.hand + q, W.hstride, s, P, delta);
-    const bool cast = !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f);  // see sample_color
-    W.scol[e] = make_float4(c.x, c.y, c.z, u2f(cast ? 1u : 0u));
-    if (cast) {
-        W.sray[e] = make_float4(P.x, P.y, P.z, 0.0f);
-        W.sray[W.sstride + e] = make_float4(delta.x, delta.y, delta.z, 0.0f);
-    }
-}
-
-template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256) void k_shadow_cast(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths;
-    if (!CHAIN) count = level_range(W, L).count;
-    ShadowSrc src{W};
-    persistent_cast<PF, true>(S, W.qctr + 32 + L, count * (uint32_t)W.group, 0.0001, 1, false, src);
-}
-
-// colorFromLights' sums of k_shadow from the stored sample colours (shadowed: +0)
-template <bool CHAIN>
-__global__ __launch_bounds__(256) void k_shadow_sum(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
-    const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t q = e / G, s = e % G;
-    const bool in = q < count;
-    const uint32_t i = base + (in ? q : 0u);
-    const float4 nd = W.node[i];
-    const bool lit = in && (f2u(nd.w) & INFO_LIT);
-    F3 c = f3(0, 0, 0);
-    if (lit && s < ns) {
-        const float4 v = W.scol[e];
-        if (f2u(v.w) != 2u) c = f3(v.x, v.y, v.z);
-    }
-    const F3 ret = light_sums(S, G, f3(nd.x, nd.y, nd.z), c);
-    if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
 
 // tree schedule: surface + children, bottom-up into the parent's child slot (materials.js:277-330)
@@ -860,8 +151,6 @@ __global__ __launch_bounds__(256) void k_final(RenderArgs A, int32_t passes) {
 // ---------------------------------------------------------------------------------------------
 // host orchestration
 namespace {
-inline unsigned grid(size_t n) { return (unsigned)((n + 255) / 256); }
-
 template <class T>
 T *carve(uint8_t *&p, size_t n) {
     T *r = reinterpret_cast<T *>(p);
@@ -938,85 +227,51 @@ Wavefront::~Wavefront() {
     if (mem) (void)hipFree(mem);
 }
 
-namespace {
-inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 255) / 256); }
 
 // Grid of a persistent kernel: as many 256-thread blocks as the device keeps resident (occupancy x
-// CUs), never more than the work needs.  Cached per kernel and device.
+// CUs), never more than the work needs.  Cached per kernel and device behind a mutex: renders run
+// concurrently on several host threads (Node async work, worker threads, one scene per thread).
 unsigned persistent_grid(const void *kernel, size_t work) {
+    static std::mutex mu;
     static std::vector<std::pair<std::pair<const void *, int>, unsigned>> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
     unsigned resident = 0;
-    for (auto &c : cache)
-        if (c.first.first == kernel && c.first.second == dev) resident = c.second;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto &c : cache)
+            if (c.first.first == kernel && c.first.second == dev) resident = c.second;
+    }
     if (!resident) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
         resident = (unsigned)(per_cu * cus);
+        std::lock_guard<std::mutex> lk(mu);
         cache.push_back({{kernel, dev}, resident});
     }
     return std::max(1u, std::min(resident, grid_ub(work)));
 }
 
-// Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.
-// Tree: level L's launches cover bound[L] rays (the real count is on the device and surplus
-// blocks exit at once; a count above the bound sets LVL_UNDER and the frame is redone);
-// levels are reduced bottom-up afterwards.
-template <int PF, bool CHAIN>
-void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
-               const std::vector<size_t> &bound) {
-    auto timed = [&](int which, auto launch) {
-        const bool ev = kt && kt->on(which);
-        if (ev) kt->ev[which].begin(st);
-        launch();
-        if (ev) kt->ev[which].end(st);
-    };
-    // dynamic LDS of the casting kernels: the BVH traversal stack (bvh_cast), 256 lanes x entries
-    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? (size_t)S.bvh_stack * 256 * sizeof(int) : 0;
-    // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
-    const bool Q = (PF & PF_SDF) && W.sstride != 0;
-    if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
-    timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
-    std::vector<size_t> ubs;  // launch bound of each level's ray count
-    for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
-        const size_t ub = CHAIN ? (size_t)W.npaths : bound[L];
-        ubs.push_back(ub);
-        const int child_depth = A.max_depth - L - 1;
-        timed(KT_EXTEND, [&] {
-            if (Q)
-                hipLaunchKernelGGL((k_extend_q<PF, CHAIN>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN>, ub)),
-                                   dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
-            else
-                hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
-        });
-        timed(KT_SHADE, [&] {
-            hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
-        });
-        if (W.ns > 0)
-            timed(KT_SHADOW, [&] {
-                const size_t ne = ub * (size_t)W.group;
-                if (Q && W.ns <= 64) {
-                    hipLaunchKernelGGL((k_shadow_prep<PF, CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
-                    hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN>), dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN>, ne)),
-                                       dim3(256), 0, st, S, W, L);
-                    hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
-                } else if (W.ns <= 64)
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
-                else
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
-            });
-    }
-    if (CHAIN) {
-        timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
-        return;
-    }
-    for (int L = (int)ubs.size() - 1; L >= 0; --L)
-        timed(KT_REDUCE, [&] { hipLaunchKernelGGL(k_reduce, dim3(grid_ub(ubs[L])), dim3(256), 0, st, W, L); });
-    timed(KT_ACCUM, [&] { hipLaunchKernelGGL(k_accum, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
-}
+// instantiated in render_pf.hip, one translation unit per profile
+extern template void run_batch<PF_ANALYTIC, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_ANALYTIC, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_MESH, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_MESH, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_SDF, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_SDF, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_ALL, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
+extern template void run_batch<PF_ALL, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
+                                         KernelTimes *, const std::vector<size_t> &);
 
+namespace {
 template <bool CHAIN>
 void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
                   const std::vector<size_t> &bound) {
@@ -1161,13 +416,5 @@ hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st) {
     return hipGetLastError();
 }
 
-#ifdef JSRT_DBG_COUNT
-extern "C" int jsrt_debug_counters(unsigned long long *out, int n) {
-    if (n > 256) n = 256;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), n * sizeof(unsigned long long)) != hipSuccess) return -1;
-    static const unsigned long long zero[256] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), zero, sizeof zero) == hipSuccess ? 0 : -1;
-}
-#endif
 
 }  // namespace jsrt

@@ -83,7 +83,7 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     ~Wavefront();
 };
 
-enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_N };
+enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_TRACE, KT_N };
 extern const char *const KT_NAMES[KT_N];
 
 struct EventPairs {  // reusable HIP events bracketing every launch of one kernel kind

@@ -46,7 +46,7 @@ def test_library_is_gfx950(lib):
 
 
 def test_abi_version_and_helpers(lib):
-    assert lib.jsrt_abi_version() == 1
+    assert lib.jsrt_abi_version() == 2
     from jsraytracer_amd import owned_columns
     assert owned_columns(10, 0, 1) == 10
     assert owned_columns(10, 1, 3) == 3            # 1, 4, 7

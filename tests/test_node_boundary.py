@@ -43,7 +43,7 @@ def test_addon_exports(addon):
     keys, nums = r.stdout.strip().split("\n")
     assert json.loads(keys) == sorted(["sceneCreate", "sceneDestroy", "renderSync", "render", "deviceCount",
                                        "abiVersion", "ownedColumns", "attachObj"])
-    assert nums.split() == ["1", "16", "3"]
+    assert nums.split() == ["2", "16", "3"]
 
 
 def test_addon_attach_obj_matches_python_and_reference(addon, tmp_path):
