@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <functional>
@@ -60,6 +61,7 @@ struct jsrt_scene {
     int ns = 0;            // light samples per lit node
     std::mutex wf_mutex;   // guards the cached wavefront buffers
     Wavefront wf;
+    hipEvent_t wf_busy = nullptr;  // recorded after the last render that used wf (stream order for the next)
 };
 
 extern "C" {
@@ -163,10 +165,12 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
 
 void jsrt_scene_destroy(jsrt_scene *s) {
     if (!s) return;
-    if (s->dmem) {
-        (void)hipSetDevice(s->device);
-        (void)hipFree(s->dmem);
+    (void)hipSetDevice(s->device);
+    if (s->wf_busy) {
+        (void)hipEventSynchronize(s->wf_busy);
+        (void)hipEventDestroy(s->wf_busy);
     }
+    if (s->dmem) (void)hipFree(s->dmem);
     delete s;
 }
 
@@ -279,7 +283,33 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     const size_t def_paths = (s->ds.profile & (PF_BVH | PF_TRI | PF_SDF)) ? (size_t)1 << 25 : (size_t)1 << 24;
     size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : def_paths;
     if (const char *e = getenv("JSRT_MAX_PATHS")) max_paths = (size_t)atoll(e);
-    hipError_t e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
+    // The batch's state is cached per scene and sized by max_paths (render_kernel.h
+    // wavefront_bytes_per_path: ~1.8 KB per path on the tree schedule, 60 GB at 32 M paths): the
+    // default is capped at half the device memory free now, and a batch whose buffers cannot be
+    // allocated is retried at half the size (the batch size never changes a bit of the image).
+    if (!(p && p->max_paths > 0)) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+            const size_t cap = free_b / 2 / std::max<size_t>(1, wavefront_bytes_per_path(s->ds, s->ns, a.max_depth));
+            if (max_paths > cap) max_paths = std::max<size_t>((size_t)1 << 16, cap & ~(size_t)63);
+        }
+    }
+    // a previous device-side render of this scene (jsrt_render_device returns before its kernels
+    // finish) may still be using the cached buffers on another stream
+    if (wf == &s->wf && s->wf_busy) (void)hipStreamWaitEvent(stream, s->wf_busy, 0);
+    hipError_t e;
+    for (;;) {
+        e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
+        if (e != hipErrorOutOfMemory || max_paths <= ((size_t)1 << 16)) break;
+        (void)hipGetLastError();
+        max_paths /= 2;
+        wf->release();
+        if (st) kt.reset();
+    }
+    if (wf == &s->wf) {
+        if (!s->wf_busy) (void)hipEventCreateWithFlags(&s->wf_busy, hipEventDisableTiming);
+        if (s->wf_busy) (void)hipEventRecord(s->wf_busy, stream);
+    }
     int rc = prev_rc;
     if (!rc && e != hipSuccess) rc = set_error(-3, std::string("render: ") + hipGetErrorString(e));
     if (!rc && st) {

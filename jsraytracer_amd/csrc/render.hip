@@ -223,8 +223,23 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     return hipSuccess;
 }
 
-Wavefront::~Wavefront() {
+void Wavefront::release() {
     if (mem) (void)hipFree(mem);
+    mem = nullptr;
+    cap_bytes = 0;
+}
+
+Wavefront::~Wavefront() { release(); }
+
+size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
+    const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = 7 * 16;
+    const bool persist = (S.profile & PF_SDF) && S.all_roots_prims;
+    size_t group = 1;
+    while ((int)group < ns && ns <= 64) group *= 2;
+    if (S.max_children <= 1)  // chain: one ray and depth nodes per path
+        return ray + (size_t)std::max(1, max_depth) * node + hand + (persist ? group * 48 : 0);
+    const size_t pool = 8, level_cap = pool / 2;  // render_frame: pool = 8 x paths, level_cap = pool / 2
+    return pool * (ray + 8 + node + 2 * 16) + level_cap * (hand + (persist ? group * 48 : 0)) + 12;
 }
 
 

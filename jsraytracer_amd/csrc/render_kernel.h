@@ -80,6 +80,7 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     // rays: ray slots; nodes: node records; hands: hand-off records; paths: root colours
     // shadow: light-sample entries of the persistent shadow casts (0 if unused)
     hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree, size_t shadow = 0);
+    void release();  // frees the buffers (the learned pool / bounds stay)
     ~Wavefront();
 };
 
@@ -114,6 +115,10 @@ struct KernelTimes {
 // (so the accumulator holds exactly the reference's sums and render_preview may publish it).
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
                         size_t max_paths, const std::function<bool(int, double, bool)> &progress);
+
+// Device bytes of the batch state per path of a batch (Wavefront::reserve for the schedule and pool
+// render_frame picks for this scene): caps the default batch size.
+size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth);
 
 // Running mean of the first `passes` samples -> A.rgba / A.colors (k_final with times(1/passes),
 // renderers.js:93-98): the image IncrementalMultisamplingRenderer holds after pass passes-1.

@@ -74,20 +74,25 @@ class HipRenderer {
     static computePixelCount(img, x_offset, x_delt) {  // renderers.js:7-9
         return ((img.width() / x_delt) + Math.round(1 - x_offset / x_delt) * (img.width() % x_delt)) * img.height();
     }
-    _params(img, timelimit, x_offset, x_delt) {
+    _params(img, timelimit, x_offset, x_delt, callback) {
         if (!(x_delt > 0)) throw "HipRenderer: x_delt must be positive";
+        // With a callback the Incremental renderer reports per pass (renderers.js:103-112): one sample
+        // per pixel per launch, so the callback sees each pass's running mean in img at the reference's
+        // cadence.  Without one, the library's batch size renders the frame in as few launches as fit.
+        const perPass = !!(timelimit && callback) && this.kind === KIND.IncrementalMultisamplingRenderer;
         return { width: img.width(), height: img.height(), samplesPerPixel: this.samplesPerPixel,
                  maxRecursionDepth: this.maxRecursionDepth, kind: this.kind, seed: this.seed,
-                 x_offset, x_delt, device: this.device, timelimit: timelimit || 0 };
+                 x_offset, x_delt, device: this.device, timelimit: timelimit || 0,
+                 samplesPerLaunch: perPass ? (this.samplesPerLaunch || 1) : 0 };
     }
     render(img, timelimit = 0, callback = false, x_offset = 0, x_delt = 1) {
-        const p = this._params(img, timelimit, x_offset, x_delt);
+        const p = this._params(img, timelimit, x_offset, x_delt, callback);
         const cb = (timelimit && callback) ? (pass, completion) => callback({ pass, completion }) : undefined;
         this.stats = addon().renderSync(this.handle, p, img.imgdata.data, cb);
         return img;
     }
     renderAsync(img, timelimit = 0, callback = false, x_offset = 0, x_delt = 1) {
-        const p = this._params(img, timelimit, x_offset, x_delt);
+        const p = this._params(img, timelimit, x_offset, x_delt, callback);
         const cb = (timelimit && callback) ? (pass, completion) => callback({ pass, completion }) : undefined;
         return addon().render(this.handle, p, img.imgdata.data, cb).then((st) => { this.stats = st; return img; });
     }

@@ -91,6 +91,7 @@ void read_params(napi_env env, napi_value o, jsrt_params *p) {
     p->device = prop_i32(env, o, "device", 0);
     p->timelimit_ms = prop_f64(env, o, "timelimit", 0);
     p->max_paths = prop_i32(env, o, "maxPaths", 0);
+    p->samples_per_launch = prop_i32(env, o, "samplesPerLaunch", 0);
 }
 
 napi_value stats_object(napi_env env, const jsrt_stats &st) {
@@ -111,6 +112,8 @@ napi_value stats_object(napi_env env, const jsrt_stats &st) {
 
 struct SceneBox {  // the external's payload: destroy is idempotent (explicit + GC finalizer)
     jsrt_scene *s = nullptr;
+    int inflight = 0;              // async renders queued or running (all counted on the JS thread)
+    bool destroy_pending = false;  // sceneDestroy while renders were in flight: destroyed by the last
 };
 void box_finalize(napi_env, void *data, void *) {
     SceneBox *b = static_cast<SceneBox *>(data);
@@ -150,8 +153,12 @@ napi_value SceneDestroy(napi_env env, napi_callback_info info) {
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     SceneBox *b = argc ? get_scene(env, argv[0]) : nullptr;
     if (b && b->s) {
-        jsrt_scene_destroy(b->s);
-        b->s = nullptr;
+        if (b->inflight > 0) {  // the scene is in use by queued / running async renders
+            b->destroy_pending = true;
+        } else {
+            jsrt_scene_destroy(b->s);
+            b->s = nullptr;
+        }
     }
     return nullptr;
 }
@@ -175,7 +182,7 @@ napi_value RenderSync(napi_env env, napi_callback_info info) {
     napi_value argv[4];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     SceneBox *b = argc > 0 ? get_scene(env, argv[0]) : nullptr;
-    if (!b || !b->s) {
+    if (!b || !b->s || b->destroy_pending) {
         napi_throw_type_error(env, "JSRT", "renderSync: scene handle is missing or destroyed");
         return nullptr;
     }
@@ -217,7 +224,9 @@ struct AsyncJob {
     napi_async_work work = nullptr;
     napi_deferred deferred = nullptr;
     napi_threadsafe_function tsfn = nullptr;
-    napi_ref buf_ref = nullptr;  // keeps the output array alive while the render writes into it
+    napi_ref buf_ref = nullptr;    // keeps the output array alive while the render writes into it
+    napi_ref scene_ref = nullptr;  // keeps the scene external (and its GC finalizer) alive meanwhile
+    SceneBox *box = nullptr;
     jsrt_scene *scene = nullptr;
     jsrt_params p;
     uint8_t *rgba = nullptr;
@@ -269,6 +278,11 @@ void async_complete(napi_env env, napi_status, void *data) {
     }
     if (j->tsfn) napi_release_threadsafe_function(j->tsfn, napi_tsfn_release);
     if (j->buf_ref) napi_delete_reference(env, j->buf_ref);
+    if (j->box && --j->box->inflight == 0 && j->box->destroy_pending && j->box->s) {
+        jsrt_scene_destroy(j->box->s);  // sceneDestroy was called while this render ran
+        j->box->s = nullptr;
+    }
+    if (j->scene_ref) napi_delete_reference(env, j->scene_ref);
     napi_delete_async_work(env, j->work);
     delete j;
 }
@@ -278,7 +292,7 @@ napi_value Render(napi_env env, napi_callback_info info) {
     napi_value argv[4];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     SceneBox *b = argc > 0 ? get_scene(env, argv[0]) : nullptr;
-    if (!b || !b->s) {
+    if (!b || !b->s || b->destroy_pending) {
         napi_throw_type_error(env, "JSRT", "render: scene handle is missing or destroyed");
         return nullptr;
     }
@@ -296,6 +310,9 @@ napi_value Render(napi_env env, napi_callback_info info) {
     }
     j->rgba = static_cast<uint8_t *>(rgba);
     napi_create_reference(env, argv[2], 1, &j->buf_ref);
+    napi_create_reference(env, argv[0], 1, &j->scene_ref);
+    j->box = b;
+    ++b->inflight;
     napi_value promise, name;
     NAPI_OK(napi_create_promise(env, &j->deferred, &promise));
     napi_create_string_utf8(env, "jsrt_render", NAPI_AUTO_LENGTH, &name);

@@ -147,7 +147,10 @@ class HipRenderer:
         progress = None
         spl = 0
         if timelimit and callback:
-            spl = max(1, self.samplesPerPixel // 8)  # progressive launches so the cadence is observable
+            # the Incremental renderer reports per pass (renderers.js:103-112): one sample per pixel per
+            # launch, so each callback sees that pass's running mean in img; other kinds report on the
+            # library's batches
+            spl = 1 if self.kind == RENDERER_KINDS["IncrementalMultisamplingRenderer"] else 0
 
             def progress(p, c):
                 callback({"pass": p, "completion": c})

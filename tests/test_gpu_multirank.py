@@ -1,0 +1,62 @@
+"""The multi-GPU tile path with real HIP tiles: 2 rank processes on device 0 (RCCL refuses two ranks on
+one GPU, so the gather runs over gloo here; bench.py uses the nccl backend = RCCL over xGMI across GPUs).
+
+Each rank renders its 16-column blocks with jsrt_render_device (the bench's step), hands the tile to
+FrameGather, and rank 0 composites.  The result must be bit-equal to a 1-rank render of the same
+frame -- the reference's column split across workers (src/raytrace_launcher.js:65-101,
+src/renderers.js:88) composited by the main thread (raytrace_launcher.js:92-97)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W, H, SPP, DEPTH = 256, 192, 8, 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, cb, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import jsraytracer_amd as jr
+    from jsraytracer_amd.tiles import FrameGather
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    fg = FrameGather(W, H, rank, world, cb)  # host tiles: gloo gathers CPU tensors
+    dev = torch.zeros(fg.maxcols * H, dtype=torch.int32, device="cuda:0")
+    sc.render_device(dev.data_ptr(), col_block=cb, width=W, height=H, spp=SPP, max_depth=DEPTH, kind=1, seed=1,
+                     x_offset=rank, x_delt=world, stats=False)
+    torch.cuda.synchronize()
+    fg.local.copy_(dev.cpu())
+    img = fg.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "composite.npy"), FrameGather.to_rgba8(img))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 16), (3, 8)])
+def test_gpu_rank_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    mp.start_processes(_rank, args=(world, _free_port(), cb, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    comp = np.load(os.path.join(tmp_path, "composite.npy"))
+    full, _, _ = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0).render(W, H, SPP, DEPTH, 1, 1,
+                                                                                     want_colors=False)
+    assert np.array_equal(comp, full)

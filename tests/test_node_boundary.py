@@ -162,3 +162,59 @@ def test_live_scene_graph_export_matches_committed_blob(addon):
     assert lines[0] == "same"
     from jsraytracer_amd import _native
     assert lines[1] == ("created" if _native.lib().jsrt_device_count() > 0 else "jsrt_scene_create")
+
+
+@pytest.mark.gpu
+def test_node_progress_per_pass_running_mean(addon, tmp_path):
+    """renderers.js:103-112 on the reference's own runtime: HipRenderer.render(img, timelimit, cb) on the
+    Incremental renderer fires callback({pass, completion}) per pass with completion increasing, and the
+    img the callback sees holds the running mean of passes 0..pass -- the spp = pass+1 frame."""
+    import jsraytracer_amd as jr
+    W, H, spp = 40, 32, 5
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "cornell_box_path.jsrt.gz")
+    code = ("const fs=require('fs'),z=require('zlib');"
+            "const {HipRenderer,NodePixelBuffer}=require('./jsraytracer_amd/js/hip_renderer');"
+            f"const b=new Uint8Array(z.gunzipSync(fs.readFileSync({json.dumps(scene)})));"
+            f"const r=new HipRenderer(b,{{samplesPerPixel:{spp},maxRecursionDepth:8,seed:5}});"
+            f"const img=new NodePixelBuffer({W},{H}); const seen=[];"
+            "r.render(img, 1e-9, (p)=>{seen.push(p); fs.writeFileSync("
+            f"{json.dumps(str(tmp_path))}+'/pass'+p.pass+'.rgba', Buffer.from(img.imgdata.data));}});"
+            f"fs.writeFileSync({json.dumps(str(tmp_path))}+'/final.rgba', Buffer.from(img.imgdata.data));"
+            "console.log(JSON.stringify(seen)); r.destroy();")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    seen = json.loads(r.stdout.strip().split("\n")[-1])
+    assert [s["pass"] for s in seen] == list(range(spp - 1))  # the last pass is the final image
+    comp = [s["completion"] for s in seen]
+    assert comp == sorted(comp) and all(0 < c < 1 for c in comp)
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    for s in seen:
+        got = np.fromfile(tmp_path / f"pass{s['pass']}.rgba", np.uint8).reshape(H, W, 4)
+        ref, _, _ = sc.render(W, H, s["pass"] + 1, 8, 1, 5, want_colors=False)
+        assert np.array_equal(got, ref), f"pass {s['pass']}"
+    final = np.fromfile(tmp_path / "final.rgba", np.uint8).reshape(H, W, 4)
+    assert np.array_equal(final, sc.render(W, H, spp, 8, 1, 5, want_colors=False)[0])
+
+
+@pytest.mark.gpu
+def test_node_destroy_while_async_render_in_flight(addon):
+    """sceneDestroy (HipRenderer.destroy) right after an un-awaited renderAsync: the render keeps its
+    scene alive and completes correctly; the scene is destroyed after it, and a new render throws."""
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "ASimpleScene.jsrt.gz")
+    tag = "ASimpleScene_incremental_64x64_s1_d4_seed1"
+    code = ("const fs=require('fs'),z=require('zlib');"
+            "const {HipRenderer,NodePixelBuffer}=require('./jsraytracer_amd/js/hip_renderer');"
+            f"const b=new Uint8Array(z.gunzipSync(fs.readFileSync({json.dumps(scene)})));"
+            "const r=new HipRenderer(b,{samplesPerPixel:1,maxRecursionDepth:4,seed:1});"
+            "const img=new NodePixelBuffer(64,64); const p=r.renderAsync(img); r.destroy();"
+            "p.then(()=>{ let t='no throw'; try { r.render(img); } catch(e) { t='throws'; }"
+            "process.stdout.write(Buffer.from(img.imgdata.data).toString('base64')+'\\n'+t+'\\n'); })"
+            ".catch(e=>{console.error(e); process.exit(1);});")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    data, thrown = r.stdout.strip().split("\n")
+    import base64
+    got = np.frombuffer(base64.b64decode(data), np.uint8).reshape(64, 64, 4)
+    _, grgba = pyoracle.golden_image(tag, 64, 64)
+    assert np.array_equal(got, grgba)
+    assert thrown == "throws"
