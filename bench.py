@@ -247,9 +247,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # JSRT_BENCH_BACKEND=gloo rehearses the N > 1 path on fewer GPUs than ranks (ranks share devices
+    # round-robin, tiles are gathered through host memory); the bench proper uses nccl = RCCL over xGMI
+    backend = os.environ.get("JSRT_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import jsraytracer_amd as jr
     from jsraytracer_amd.tiles import FrameGather
@@ -274,16 +282,20 @@ def main():
     t_upload = time.perf_counter() - t_load - t_build
 
     cb = args.col_block if world > 1 else 1
-    fg = FrameGather(W, H, rank, world, cb, device=f"cuda:{local}")
+    host_tiles = world > 1 and backend != "nccl"
+    fg = FrameGather(W, H, rank, world, cb, device="cpu" if host_tiles else f"cuda:{local}")
+    tile = torch.zeros_like(fg.local, device=f"cuda:{local}") if host_tiles else fg.local
     stream = torch.cuda.current_stream().cuda_stream
     STAGES = jr._native.STAGES
 
     def step(events=None, colors=None):
         """events: None = no HIP events; 0 = every stage; else a bitmask of stages (jsrt.h stage_events)."""
-        st = scene.render_device(fg.local.data_ptr(), colors.data_ptr() if colors is not None else None,
+        st = scene.render_device(tile.data_ptr(), colors.data_ptr() if colors is not None else None,
                                  stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp, max_depth=depth,
                                  kind=kind, seed=1, x_offset=rank if world > 1 else 0, x_delt=world,
                                  stats=events is not None, stage_events=events or 0)
+        if host_tiles:
+            fg.local.copy_(tile.cpu())
         fg.gather()
         return st
 
@@ -303,7 +315,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host_tiles else f"cuda:{local}")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
@@ -353,7 +365,8 @@ def main():
             "data": "reference scene graph (exported from the live reference, not synthetic), keyed RNG seed 1",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth} (Incremental)", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"tiles{world}",
-                       "col_block": cb, "headline": args.config == HEADLINE and args.spp == 0},
+                       "col_block": cb, "headline": args.config == HEADLINE and args.spp == 0,
+                       "gather_backend": backend if world > 1 else None},
             "roofline": roof, "cpu_baseline": cpu, "parity": par,
             "kernel_ms_per_step": kernel_ms,
             "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
