@@ -147,6 +147,67 @@ __device__ __forceinline__ bool aabb_slab(float cx, float cy, float cz, float hx
     return true;
 }
 
+// The BVH entry test (aggregates.js:208-209: AABB.get_intersects, then ts.min <= maxD, ts.max >= minD,
+// ts.min <= ret.distance) evaluated in f32 with an error bound; only a decision too close to call runs
+// the exact f64 slab (aabb_slab: six correctly rounded divisions).
+//
+// Exactness: the reference's result is a boolean of comparisons between the quotients (p_i +- h_i) /
+// d_i (f64, p = center - origin in f32 as Vec.minus stores it) and the doubles minD, lim =
+// min(maxD, best).  Swaps, running max / min and the per-axis early outs reduce to: enter iff every
+// skipped axis (|d_i| <= 1e-7) has |p_i| <= h_i, and max_i lo_i <= min_i hi_i, min_i hi_i >= minD,
+// max_i lo_i <= lim.  Here each quotient is (p_i +- h_i) * (1 / d_i) in f32: within 3 f32 roundings
+// (3u, u = 2^-24) of the real quotient, which the f64 quotient is within 2^-53 of.  A comparison is
+// decided only when its operands are apart by more than EPS = 2^-21 (> 8u) of their magnitudes
+// (+ 1e-30 absolute, for underflow); then it has the exact outcome.  Overflow / NaN is "too close".
+struct BoxRay {       // per ray: the f32 reciprocals and the reference's epsilon test per axis
+    float inv[3];
+    uint32_t skip;    // bit i: |d_i| <= 1e-7 (geometry.js:194, compared in f64)
+};
+__device__ __forceinline__ BoxRay box_ray(F3 d) {
+    BoxRay r;
+    const float dd[3] = {d.x, d.y, d.z};
+    r.skip = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const bool sk = !(fabs((double)dd[i]) > 0.0000001);
+        r.skip |= (sk ? 1u : 0u) << i;
+        r.inv[i] = sk ? 0.0f : 1.0f / dd[i];
+    }
+    return r;
+}
+// 1: enter, 0: skip, -1: too close to call (run the exact test)
+__device__ __forceinline__ int box_enter_f32(float cx, float cy, float cz, float hx, float hy, float hz, F3 o,
+                                             const BoxRay &r, float fmin_d, float flim) {
+    constexpr float EPS = 4.76837158203125e-7f, TINY = 1e-30f;  // 2^-21
+    const float c[3] = {cx, cy, cz}, h[3] = {hx, hy, hz}, oo[3] = {o.x, o.y, o.z};
+    float tmin = -__builtin_inff(), tmax = __builtin_inff();
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float p = c[i] - oo[i];
+        if ((r.skip >> i) & 1u) {
+            out = out || fabsf(p) > h[i];  // exact: both f32
+        } else {
+            const float a = (p + h[i]) * r.inv[i], b = (p - h[i]) * r.inv[i];
+            tmin = fmaxf(tmin, fminf(a, b));
+            tmax = fminf(tmax, fmaxf(a, b));
+        }
+    }
+    if (out) return 0;
+    if (r.skip == 7u) return 1;  // no slab: (-inf, inf) always enters
+    // finite unless an axis overflowed (a skipped axis never sets them, a used one always does)
+    if (!__builtin_isfinite(tmin) || !__builtin_isfinite(tmax)) return -1;
+    const float en = EPS * fabsf(tmin) + TINY, ex = EPS * fabsf(tmax) + TINY;
+    const float em = EPS * fabsf(fmin_d) + TINY;
+    // c1: tmin <= tmax, c2: tmax >= minD, c3: tmin <= lim (lim may be +inf: always true)
+    if (tmin - en > tmax + ex || tmax + ex < fmin_d - em) return 0;
+    const bool c3_true = !__builtin_isfinite(flim) ? flim > 0 : tmin + en < flim - (EPS * fabsf(flim) + TINY);
+    const bool c3_false = __builtin_isfinite(flim) ? tmin - en > flim + (EPS * fabsf(flim) + TINY) : flim < 0;
+    if (c3_false) return 0;
+    if (tmin + en < tmax - ex && tmax - ex > fmin_d + em && c3_true) return 1;
+    return -1;
+}
+
 __device__ __forceinline__ double plane_t(F3 o, F3 d) {  // geometry.js:246-248
     return (d.z != 0.0f) ? -(double)o.z / (double)d.z : -DINF;
 }
@@ -550,15 +611,26 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
     extern __shared__ int bvh_lds_stack[];
     int *const stack = bvh_lds_stack + threadIdx.x;
     const int stride = (int)blockDim.x;
+    const BoxRay br = box_ray(d);
+    const float fmin_d = (float)minD;
+    float flim = (float)maxD;  // (float)min(maxD, best)
     int sp = 0;
     stack[0] = I.first;
     ++sp;
     while (sp > 0) {
         --sp;
         const DBvhNode N = S.bvh[stack[sp * stride]];
-        double tmn, tmx;
-        if (aabb_slab(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, d, minD, maxD, tmn, tmx) && tmn <= maxD && tmx >= minD &&
-            tmn <= best.t) {
+#ifndef JSRT_NO_BOX_FILTER
+        int en = box_enter_f32(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, br, fmin_d, flim);
+#else
+        int en = -1;
+#endif
+        if (en < 0) {
+            double tmn, tmx;
+            en = aabb_slab(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, d, minD, maxD, tmn, tmx) && tmn <= maxD &&
+                 tmx >= minD && tmn <= best.t;
+        }
+        if (en) {
             if (N.b < 0) {
                 const int cnt = ~N.b;
                 for (int k = 0; k < cnt; ++k) {
@@ -569,6 +641,7 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                         best.t = t;
                         best.prim = S.leaf_prims[N.a + k];
                         if (ANY) return best;
+                        flim = (float)fmin(maxD, best.t);
                     }
                 }
             } else {
