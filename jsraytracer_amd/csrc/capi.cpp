@@ -109,7 +109,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
                  o_roots = A.add(H.roots), o_rb = A.add(H.rbounds), o_rr = A.add(H.rootrec), o_mats = A.add(H.mats), o_ctx = A.add(H.ctx), o_bvh = A.add(H.bvh),
                  o_lp = A.add(H.leaf_prims), o_lt = A.add(H.leaf_tris), o_tris = A.add(H.tris),
                  o_trish = A.add(H.trish), o_mat = A.add(H.mat), o_matf = A.add(H.mat_flags), o_ps = A.add(H.prim_shade),
-                 o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_lights = A.add(H.lights),
+                 o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_mcc = A.add(H.mc_const), o_lights = A.add(H.lights),
                  o_sl = A.add(H.sample_light), o_sc = A.add(H.sample_call),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
                  o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg);
@@ -138,6 +138,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.shade0 = (const double *)(b + o_sh0);
     D.shadeI = (const double *)(b + o_shI);
     D.mc = (const jsrt_rec_mcolor *)(b + o_mc);
+    D.mc_const = (const float *)(b + o_mcc);
     D.lights = (const DLight *)(b + o_lights);
     D.sample_light = (const int32_t *)(b + o_sl);
     D.sample_call = (const int32_t *)(b + o_sc);

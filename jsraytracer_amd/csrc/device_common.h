@@ -910,6 +910,12 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
 // --------------------------------------------------------------------------------------------
 // materials (materials.js)
 __device__ __forceinline__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
+#ifndef JSRT_AB_MC_WALK
+    {  // a chain that does not read (u, v): its colour, computed by the loader (scene_load.cpp mc_constants)
+        const float4 cc = *reinterpret_cast<const float4 *>(S.mc_const + 4 * m);
+        if (cc.w != 0.0f) return f3(cc.x, cc.y, cc.z);
+    }
+#endif
     // walk Scaled* wrappers (and checkerboard choices) down to the solid colour, then apply the
     // scales innermost first: ScaledMaterialColor.color = child.color(data).times(scale)
     auto step = [&](int x) {  // next record below x (checkerboards resolved by (u, v))

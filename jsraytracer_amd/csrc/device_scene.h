@@ -129,6 +129,7 @@ struct DScene {
     const double *shade0;        // 16 per slot: prim.inv x identity (the ctx-0 shading matrix)
     const double *shadeI;        // 16 per ctx: identity x ctx (shading matrix of identity prims)
     const jsrt_rec_mcolor *mc;
+    const float *mc_const;       // 4 per mc record: xyz its colour when UV-independent (w = 1)
     const DLight *lights;
     const SdfInsn *sdf_insn;     // SDF programs (sdf_program.h)
     const double *sdf_const;

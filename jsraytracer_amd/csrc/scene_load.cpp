@@ -680,6 +680,36 @@ struct Loader {
         }
     }
 
+    // MaterialColor.color(data) of every colour chain that does not read (u, v) (no checkerboard):
+    // mc_eval's arithmetic (device_common.h) done once here -- the solid colour, then the Scaled
+    // wrappers innermost first, f32(x * s) in f64 for a scalar, f32 products for a vector -- so the
+    // kernels read one record instead of walking the chain with dependent loads.
+    void mc_constants() {
+        S.mc_const.assign(4 * S.mc.size(), 0.0f);
+        for (size_t x = 0; x < S.mc.size(); ++x) {
+            if (mc_uses_uv((int32_t)x)) continue;
+            std::vector<int32_t> wrap;  // Scaled wrappers from the top down
+            int32_t y = (int32_t)x;
+            bool ok = true;
+            for (int g = 0; g < 16 && ok && S.mc[y].kind != JSRT_MC_SOLID; ++g) {
+                const uint32_t k = S.mc[y].kind;
+                ok = (k == JSRT_MC_SCALED_SCALAR || k == JSRT_MC_SCALED_VEC) && S.mc[y].a >= 0 &&
+                     (size_t)S.mc[y].a < S.mc.size();
+                wrap.push_back(y);
+                if (ok) y = S.mc[y].a;
+            }
+            if (!ok || S.mc[y].kind != JSRT_MC_SOLID) continue;
+            float c[3] = {S.mc[y].vec[0], S.mc[y].vec[1], S.mc[y].vec[2]};
+            for (size_t i = wrap.size(); i-- > 0;) {
+                const jsrt_rec_mcolor &M = S.mc[wrap[i]];
+                for (int k = 0; k < 3; ++k)
+                    c[k] = M.kind == JSRT_MC_SCALED_SCALAR ? (float)((double)c[k] * M.scalar) : c[k] * M.vec[k];
+            }
+            memcpy(&S.mc_const[4 * x], c, sizeof c);
+            S.mc_const[4 * x + 3] = 1.0f;
+        }
+    }
+
     // Area light world normal: inv_transform.transposed().times(n).to4(0).normalized() (lights.js:90)
     void area_normal(const double *Ti, float *out) {
         const double n[4] = {0, 0, 1, 0};
@@ -734,6 +764,7 @@ struct Loader {
             S.mat_flags.push_back(fl);
         }
         for (uint32_t i = 0; i < B.n_mc; ++i) S.mc.push_back(B.mc[i]);
+        mc_constants();
 
         const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
         for (int k = 0; k < 16; ++k) S.ctx.push_back(I[k]);  // ctx 0: World.color's Mat4.identity()

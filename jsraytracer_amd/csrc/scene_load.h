@@ -25,6 +25,7 @@ struct HostScene {
     std::vector<int32_t> prim_shade;   // -1: identity inv_transform; else slot in shade0
     std::vector<double> shade0, shadeI;  // 16 per slot / per ctx: precomputed shading matrices
     std::vector<jsrt_rec_mcolor> mc;
+    std::vector<float> mc_const;        // 4 per mc record: its colour when UV-independent (w = 1), else w = 0
     std::vector<DLight> lights;
     std::vector<int32_t> sample_light, sample_call;  // per light sample of a node
     int32_t light_draws = 0;
