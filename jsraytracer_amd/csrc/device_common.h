@@ -101,7 +101,8 @@ __device__ __forceinline__ double average3(F3 a) {  // Vec.average (math.js:261-
 }
 
 // Mat(3x4 rows, implicit row 3 = 0,0,0,1) * Vec (math.js:392-397): f64 dot in order, f32 store.
-__device__ __forceinline__ F3 xf_point(const double *m, F3 o) {  // w = 1
+template <class T>
+__device__ __forceinline__ F3 xf_point(const T *m, F3 o) {  // w = 1 (T: double in any address space)
     return f3((float)((((double)o.x * m[0] + (double)o.y * m[1]) + (double)o.z * m[2]) + m[3]),
               (float)((((double)o.x * m[4] + (double)o.y * m[5]) + (double)o.z * m[6]) + m[7]),
               (float)((((double)o.x * m[8] + (double)o.y * m[9]) + (double)o.z * m[10]) + m[11]));
@@ -244,6 +245,41 @@ __device__ __forceinline__ double tri_intersect(const DTri &T, F3 o, F3 d) {  //
 // branch.  The stacks are small fixed register files indexed by those uniform values.
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// read-only scene data addressed by a wave-uniform index, viewed in the constant address space so the
+// compiler may load it with scalar loads (generic pointers get per-lane vector loads)
+#define CONST_AS __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const CONST_AS T *as_const(const T *p) {
+    return (const CONST_AS T *)p;
+}
+
+// BoxSDF.distanceComp (sdf.js:276-279): q = p.abs().minus(size).to4(0);
+// Vec.max(q, 0).norm() + min(max(q0, q1, q2), 0)
+template <class T>
+__device__ __forceinline__ double sdf_box(const T *k, F3 P) {
+    const float qx = fabsf(P.x) - (float)k[0];
+    const float qy = or0(fabsf(P.y) - (float)k[1]);
+    const float qz = or0(fabsf(P.z) - (float)k[2]);
+    const F3 m = f3((float)js_max(qx, 0), (float)js_max(qy, 0), (float)js_max(qz, 0));
+    return sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0);
+}
+
+// SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473): Math.fmod(p + s/2, s) - s/2 per axis.
+// k[3..5]: 1/s when s is a power of two (x / s and x * (1 / s) are then the same rounding of the
+// same real number), else 0.
+template <class T>
+__device__ __forceinline__ F3 sdf_xrep(const T *k, F3 P) {
+    const float pc[3] = {P.x, P.y, P.z};
+    float r[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double s = k[i], inv = k[3 + i], a = (double)pc[i] + s / 2;
+        const double q = floor(inv != 0.0 ? a * inv : a / s);
+        r[i] = (float)(to_precision8(a - (q * s)) - s / 2);  // math.js:27
+    }
+    return f3(r[0], or0(r[1]), or0(r[2]));
+}
+
 template <int N>
 struct RegFile {  // per-lane doubles addressed by a wave-uniform index
     double r[N];
@@ -267,24 +303,23 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
     F3 pst0 = P, pst1 = P;  // SDF_MAX_P == 2
     int lc0 = 0, lc1 = 0;   // SDF_MAX_LOOP == 2
     int dsp = 0, psp = 0, ssp = 0, lsp = 0;
+#ifndef JSRT_AB_FLAT_VM
+    // The program and its constants are read-only and every index is wave-uniform: through the
+    // constant address space the loads are scalar (s_load, scalar cache) instead of a vector load per
+    // lane on the interpreter's dependent chain.
+    const CONST_AS SdfInsn *code = as_const(S.sdf_insn);
+    const CONST_AS double *K = as_const(S.sdf_const);
+#else
     const SdfInsn *code = S.sdf_insn;
     const double *K = S.sdf_const;
+#endif
     pc = uni(pc);  // uniform among the active lanes (sdf_node_dist's waterfall)
     end = uni(end);
     while (pc < end) {
-        const SdfInsn I = code[pc];
-        const int op = uni(I.op), ia = uni(I.a), ib = uni(I.b);
+        const int op = uni(code[pc].op), ia = uni(code[pc].a), ib = uni(code[pc].b);
         switch (op) {
         case SOP_END: pc = end; continue;
-        case SOP_BOX: {  // BoxSDF.distanceComp (sdf.js:276-279)
-            // q = p.abs().minus(size).to4(0); Vec.max(q, 0).norm() + min(max(q0,q1,q2), 0)
-            const float qx = fabsf(P.x) - (float)K[ia];
-            const float qy = or0(fabsf(P.y) - (float)K[ia + 1]);
-            const float qz = or0(fabsf(P.z) - (float)K[ia + 2]);
-            const F3 m = f3((float)js_max(qx, 0), (float)js_max(qy, 0), (float)js_max(qz, 0));
-            dst.set(dsp++, sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0));
-            break;
-        }
+        case SOP_BOX: dst.set(dsp++, sdf_box(K + ia, P)); break;
         case SOP_SPHERE: {  // p.to4(0).norm() - radius (sdf.js:232-234)
             const F3 q = f3(P.x, or0(P.y), or0(P.z));
             dst.set(dsp++, sqrt(dot3(q, q)) - K[ia]);
@@ -343,12 +378,27 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
             if (dt < 0) P = sub(P, scale(n, 2 * dt));
             break;
         }
-        case SOP_XREP: {  // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473)
-            const double sx = K[ia], sy = K[ia + 1], sz = K[ia + 2];
-            const float x = (float)(js_fmod((double)P.x + sx / 2, sx) - sx / 2);
-            const float y = (float)(js_fmod((double)P.y + sy / 2, sy) - sy / 2);
-            const float z = (float)(js_fmod((double)P.z + sz / 2, sz) - sz / 2);
-            P = f3(x, or0(y), or0(z));
+        case SOP_XREP: P = sdf_xrep(K + ia, P); break;
+        case SOP_MINBOX: {  // BOX x ib, MIN ib
+            double r = sdf_box(K + ia, P);
+            for (int i = 1; i < ib; ++i) r = js_min(r, sdf_box(K + ia + 4 * i, P));
+            dst.set(dsp++, r);
+            break;
+        }
+        case SOP_XMATS:  // TPUSH XMAT TPOP_MUL
+            P = xf_point(K + ia, P);
+            sst.set(ssp - 1, sst.get(ssp - 1) * (1.0 * K[ib]));
+            break;
+        case SOP_XMATREP: {  // TPUSH XMATS XREP TPOP_MUL
+            const int ic = uni(code[pc].pad);
+            P = sdf_xrep(K + ic, xf_point(K + ia, P));
+            sst.set(ssp - 1, sst.get(ssp - 1) * (1.0 * (1.0 * K[ib])));
+            break;
+        }
+        case SOP_MULSMIN: {  // MULS, MIN 2
+            const double d = dst.get(dsp - 1) * sst.get(ssp - 1);
+            --dsp;
+            dst.set(dsp - 1, js_min(dst.get(dsp - 1), d));
             break;
         }
         case SOP_LOOP:

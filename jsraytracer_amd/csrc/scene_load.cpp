@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <map>
+#include <set>
 #include <unordered_map>
 
 namespace jsrt {
@@ -440,7 +441,15 @@ struct Loader {
             if (N.vec[3] != 0.0f) fail("reflection normal must have w = 0");
             emit(SOP_XREF, kconst({N.vec[0], N.vec[1], N.vec[2], N.k}));
             break;
-        case JSRT_SDFT_REPETITION: emit(SOP_XREP, kconst({N.vec[0], N.vec[1], N.vec[2]})); break;
+        case JSRT_SDFT_REPETITION: {  // + the exact reciprocal of a power-of-two size (x / s == x * (1 / s))
+            auto rcp2 = [](double v) {
+                int e;
+                const double m = frexp(v, &e);
+                return (isfinite(v) && fabs(m) == 0.5) ? 1.0 / v : 0.0;
+            };
+            emit(SOP_XREP, kconst({N.vec[0], N.vec[1], N.vec[2], rcp2(N.vec[0]), rcp2(N.vec[1]), rcp2(N.vec[2])}));
+            break;
+        }
         default: fail("unsupported SDF transformer");
         }
     }
@@ -545,6 +554,63 @@ struct Loader {
         }
         if (md > SDF_MAX_D || mp > SDF_MAX_P || ms > SDF_MAX_S || ml > SDF_MAX_LOOP)
             fail("SDF tree too deep/wide for the GPU program stacks");
+    }
+
+    // Peephole fusion of a compiled range into one-dispatch forms (sdf_program.h); returns the fused
+    // range appended to the program.  Every fused op performs the same IEEE operations in the same
+    // order as the sequence it replaces; only scale multiplies by an exact 1.0 (a transformer that
+    // does not scale) are dropped.  LOOP / ENDLOOP targets are remapped.
+    std::pair<int32_t, int32_t> fuse_sdf(int32_t begin, int32_t end) {
+        std::vector<SdfInsn> in(S.sdf_insn.begin() + begin, S.sdf_insn.begin() + end);
+        std::vector<int32_t> origin(in.size());  // original index of each instruction (loops)
+        for (size_t i = 0; i < in.size(); ++i) origin[i] = begin + (int32_t)i;
+        for (bool changed = true; changed;) {
+            changed = false;
+            std::vector<SdfInsn> out;
+            std::vector<int32_t> og;
+            for (size_t i = 0; i < in.size();) {
+                auto op = [&](size_t k) { return k < in.size() ? in[k].op : -1; };
+                if (op(i) == SOP_TPUSH && (op(i + 1) == SOP_XREP || op(i + 1) == SOP_XREF) && op(i + 2) == SOP_TPOP_MUL) {
+                    out.push_back(in[i + 1]), og.push_back(-1), i += 3, changed = true;  // top * 1.0: exact
+                    continue;
+                }
+                if (op(i) == SOP_TPUSH && op(i + 1) == SOP_XMAT && op(i + 2) == SOP_TPOP_MUL) {
+                    out.push_back(SdfInsn{SOP_XMATS, in[i + 1].a, in[i + 1].b, 0}), og.push_back(-1), i += 3, changed = true;
+                    continue;
+                }
+                if (op(i) == SOP_TPUSH && op(i + 1) == SOP_XMATS && op(i + 2) == SOP_XREP && op(i + 3) == SOP_TPOP_MUL) {
+                    out.push_back(SdfInsn{SOP_XMATREP, in[i + 1].a, in[i + 1].b, in[i + 2].a}), og.push_back(-1);
+                    i += 4, changed = true;
+                    continue;
+                }
+                if (op(i) == SOP_MULS && op(i + 1) == SOP_MIN && in[i + 1].a == 2) {
+                    out.push_back(SdfInsn{SOP_MULSMIN, 0, 0, 0}), og.push_back(-1), i += 2, changed = true;
+                    continue;
+                }
+                if (op(i) == SOP_BOX) {
+                    size_t n = 1;
+                    while (op(i + n) == SOP_BOX && in[i + n].a == in[i].a + 4 * (int32_t)n) ++n;
+                    if (n >= 2 && op(i + n) == SOP_MIN && in[i + n].a == (int32_t)n) {
+                        out.push_back(SdfInsn{SOP_MINBOX, in[i].a, (int32_t)n, 0}), og.push_back(-1);
+                        i += n + 1, changed = true;
+                        continue;
+                    }
+                }
+                out.push_back(in[i]), og.push_back(origin[i]), ++i;
+            }
+            in.swap(out);
+            origin.swap(og);
+        }
+        const int32_t fb = (int32_t)S.sdf_insn.size();
+        std::unordered_map<int32_t, int32_t> at;  // original index -> fused index (loop markers)
+        for (size_t i = 0; i < in.size(); ++i)
+            if (origin[i] >= 0) at[origin[i]] = fb + (int32_t)i;
+        for (SdfInsn &I : in) {
+            if (I.op == SOP_LOOP) I.b = at.at(I.b);
+            if (I.op == SOP_ENDLOOP) I.a = at.at(I.a);
+        }
+        S.sdf_insn.insert(S.sdf_insn.end(), in.begin(), in.end());
+        return {fb, (int32_t)S.sdf_insn.size()};
     }
 
     int32_t sdfg_index(int32_t g) {
@@ -871,7 +937,20 @@ struct Loader {
             S.sdf_range[2 * kv.first] = kv.second.first;
             S.sdf_range[2 * kv.first + 1] = kv.second.second;
         }
+        // a geometry's root distance (every march step, and the normal) runs its fused program;
+        // children keep their own ranges for getMaterialData (JSRT_SDF_NOFUSE=1: A/B)
+        const char *nf = getenv("JSRT_SDF_NOFUSE");
+        if (!(nf && nf[0] == '1'))
+            for (const jsrt_rec_sdfgeom &G : S.sdfg) {
+                const int32_t r = G.root;
+                if (S.sdf_range[2 * r] < 0 || fused_roots.count(r)) continue;
+                const auto fr = fuse_sdf(S.sdf_range[2 * r], S.sdf_range[2 * r + 1]);
+                S.sdf_range[2 * r] = fr.first;
+                S.sdf_range[2 * r + 1] = fr.second;
+                fused_roots.insert(r);
+            }
     }
+    std::set<int32_t> fused_roots;
 };
 
 }  // namespace

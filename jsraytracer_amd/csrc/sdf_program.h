@@ -32,9 +32,14 @@ enum SdfOp : int32_t {
     SOP_XMAT,       // a = const index of 12 doubles (inv rows 0..2), b = const of scale:
                     //   P = inv*P, top = top * scale                                   sdf.js:433-435
     SOP_XREF,       // a = const: normal xyz (f32 as double) + delta                    sdf.js:450-455
-    SOP_XREP,       // a = const: sizes xyz                                             sdf.js:471-473
+    SOP_XREP,       // a = const: sizes xyz, then 1/size (exact) or 0 per axis          sdf.js:471-473
     SOP_LOOP,       // a = iterations, b = index of the matching SOP_ENDLOOP
     SOP_ENDLOOP,    // a = index of the matching SOP_LOOP
+    // fused forms (scene_load.cpp fuse_sdf: the same operations in the same order, one dispatch)
+    SOP_MINBOX,     // BOX x b, MIN b: a = const of the first box (boxes 4 doubles apart)
+    SOP_XMATS,      // TPUSH XMAT TPOP_MUL: P = inv*P, top = top * (1 * scale)
+    SOP_XMATREP,    // TPUSH XMATS XREP TPOP_MUL: a = matrix, b = scale, pad = repetition const
+    SOP_MULSMIN,    // MULS, MIN 2: d = pop * top-scale; push Math.min(pop, d)
 };
 
 struct SdfInsn {
