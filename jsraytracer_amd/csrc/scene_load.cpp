@@ -937,20 +937,17 @@ struct Loader {
             S.sdf_range[2 * kv.first] = kv.second.first;
             S.sdf_range[2 * kv.first + 1] = kv.second.second;
         }
-        // a geometry's root distance (every march step, and the normal) runs its fused program;
-        // children keep their own ranges for getMaterialData (JSRT_SDF_NOFUSE=1: A/B)
+        // every node's distance (a geometry's root on each march step and for the normal, the children
+        // getMaterialData compares) runs a fused copy of its range (JSRT_SDF_NOFUSE=1: A/B)
         const char *nf = getenv("JSRT_SDF_NOFUSE");
         if (!(nf && nf[0] == '1'))
-            for (const jsrt_rec_sdfgeom &G : S.sdfg) {
-                const int32_t r = G.root;
-                if (S.sdf_range[2 * r] < 0 || fused_roots.count(r)) continue;
-                const auto fr = fuse_sdf(S.sdf_range[2 * r], S.sdf_range[2 * r + 1]);
-                S.sdf_range[2 * r] = fr.first;
-                S.sdf_range[2 * r + 1] = fr.second;
-                fused_roots.insert(r);
+            for (uint32_t n = 0; n < B.n_sdf; ++n) {
+                if (S.sdf_range[2 * n] < 0) continue;
+                const auto fr = fuse_sdf(S.sdf_range[2 * n], S.sdf_range[2 * n + 1]);
+                S.sdf_range[2 * n] = fr.first;
+                S.sdf_range[2 * n + 1] = fr.second;
             }
     }
-    std::set<int32_t> fused_roots;
 };
 
 }  // namespace
