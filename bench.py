@@ -268,13 +268,7 @@ def main():
         spp = args.spp
     t_load = time.perf_counter()
     if scene_name in MESH_SCENES:
-        meshes = os.path.join(ROOT, "tests", "golden", "meshes")
-        with open(os.path.join(meshes, "topology.json")) as f:
-            topo = json.load(f)[scene_name]
-        import gzip
-        with gzip.open(os.path.join(meshes, topo["skeleton"]), "rb") as f:
-            skel = f.read()
-        blob, _ = jr.load_obj_scene(skel, os.path.join(meshes, topo["obj_fixture"]))
+        blob, _ = pyoracle.mesh_scene(scene_name, jr)  # skeleton + OBJ through the native ingest
     else:
         blob = pyoracle.golden_scene(scene_name)
     t_build = time.perf_counter() - t_load

@@ -23,7 +23,16 @@
  *
  * Errors: negative return, message in jsrt_last_error of jsrt.h (the reference throws strings, e.g.
  * objloader.js:217 "Error while attempting to parse obj file on line ...", aggregates.js:39).
- * `usemtl` (MTL materials) is rejected: the native ingest takes its material from the template.
+ *
+ * jsrt_blob_attach_obj_mtl <- the same with the OBJ's mtllib files (loadMtlFiles / parseMtlFile,
+ *                           objloader.js:58-137; the text of each file in mtllib order,
+ *                           separated by NUL bytes): `usemtl`
+ *                           switches the current material to makeMaterial(newmtl block)
+ *                           (objloader.js:9-20, always a PhongMaterial: the Fresnel / path-tracing one
+ *                           is built and dropped), faces before any usemtl take the template's material
+ *                           (loadObjFile's defaultMaterial).  Without MTL text, usemtl throws "No
+ *                           material defined with name: ..." as the reference does for a missing one.
+ *                           Every BVHAggregate sharing the template tree receives the built tree.
  */
 #ifndef JSRT_MESH_H
 #define JSRT_MESH_H
@@ -51,6 +60,9 @@ typedef struct {
  * options and info may be NULL (defaults: first BVHAggregate, min_area 0.00001). */
 int jsrt_blob_attach_obj(const void *blob, size_t n, const char *obj_text, size_t obj_len,
                          const jsrt_mesh_options *options, void **out_blob, size_t *out_n, jsrt_mesh_info *info);
+int jsrt_blob_attach_obj_mtl(const void *blob, size_t n, const char *obj_text, size_t obj_len, const char *mtl_text,
+                             size_t mtl_len, const jsrt_mesh_options *options, void **out_blob, size_t *out_n,
+                             jsrt_mesh_info *info);
 void jsrt_blob_free(void *blob);
 
 #ifdef __cplusplus

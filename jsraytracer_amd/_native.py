@@ -47,7 +47,7 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_v
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_owned_columns",
            "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
-MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_free"]
+MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 
 
 class MeshOptions(ctypes.Structure):
@@ -95,6 +95,11 @@ def lib():
     L.jsrt_blob_attach_obj.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                        ctypes.POINTER(MeshOptions), ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(MeshInfo)]
+    L.jsrt_blob_attach_obj_mtl.restype = ctypes.c_int
+    L.jsrt_blob_attach_obj_mtl.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                           ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(MeshOptions),
+                                           ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                           ctypes.POINTER(MeshInfo)]
     L.jsrt_blob_free.restype = None
     L.jsrt_blob_free.argtypes = [ctypes.c_void_p]
     _lib = L

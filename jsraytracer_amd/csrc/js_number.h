@@ -79,6 +79,18 @@ __host__ __device__ inline double to_precision8_exact(double v) {
     return neg ? -r : r;
 }
 
+// 10^k exactly for 0 <= k <= 22 (5^22 < 2^53: every partial product of the binary powers is itself an
+// exact power of ten), from immediates: a per-lane table lookup would be a memory load on the SDF
+// march's dependent chain.
+__host__ __device__ inline double pow10_exact(int k) {
+    double r = (k & 1) ? 1e1 : 1.0;
+    r *= (k & 2) ? 1e2 : 1.0;
+    r *= (k & 4) ? 1e4 : 1.0;
+    r *= (k & 8) ? 1e8 : 1.0;
+    r *= (k & 16) ? 1e16 : 1.0;
+    return r;
+}
+
 // Fast path for 1e-37 <= |v| < 1e8 (every value the reference scenes produce).  The product
 // x * 10^k is carried as p + err: for k <= 22 one fma gives the exact rounding error; for k in
 // 23..44 it is x * 1e22 * 10^(k-22) in double-double (err then carries ~2^-100 relative error,
@@ -98,19 +110,17 @@ __host__ __device__ inline double to_precision8(double v) {
     int ex;
     (void)frexp(x, &ex);  // x in [2^(ex-1), 2^ex)
     int e10 = (int)floor((double)(ex - 1) * 0.30102999566398120);  // floor(log10 x) or one less
-    const double P10D[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                             1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
     for (int it = 0; it < 3; ++it) {
         const int k = 7 - e10;
         if (k > 44 && it == 0) { e10 += 1; continue; }  // the estimate may be one decade low
         if (k < 0 || k > 44) break;
         double p, err;
         if (k <= 22) {
-            const double P = P10D[k];
+            const double P = pow10_exact(k);
             p = x * P;
             err = fma(x, P, -p);
         } else {
-            const double B = P10D[k - 22];
+            const double B = pow10_exact(k - 22);
             const double p1 = x * 1e22, e1 = fma(x, 1e22, -p1);
             p = p1 * B;
             err = fma(p1, B, -p) + e1 * B;
@@ -124,11 +134,11 @@ __host__ __device__ inline double to_precision8(double v) {
         const int k2 = e - 7;
         double res;
         if (k2 >= 0) {
-            res = n * P10D[k2];  // k2 <= 0 here: e10 <= 7
+            res = n * pow10_exact(k2);  // k2 <= 0 here: e10 <= 7
         } else if (-k2 <= 22) {
-            res = n / P10D[-k2];
+            res = n / pow10_exact(-k2);
         } else {  // n / (1e22 * B): quotient and exact remainders, one final rounding
-            const double B = P10D[-k2 - 22];
+            const double B = pow10_exact(-k2 - 22);
             const double q1 = n / 1e22, r1 = fma(-q1, 1e22, n);
             const double q = q1 / B, r = fma(-q, B, q1);
             res = q + (r + r1 / 1e22) / B;

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <new>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -83,6 +84,7 @@ struct V4 {
 
 // ---------------------------------------------------------------- OBJ text -> triangles
 struct Tri {
+    int32_t mtl = -1;  // MTL material (index into the parsed list) or -1: loadObjFile's defaultMaterial
     float ps[3][4];
     int has_normal = 0, has_uv = 0, uv_len = 0;
     float vn[3][4] = {}, uv[3][4] = {};
@@ -199,8 +201,80 @@ const T &at_index(const std::vector<T> &v, double i, const char *what) {
     return v[(size_t)i];
 }
 
+// ---------------------------------------------------------------- MTL (objloader.js:58-123)
+// What makeMaterial (objloader.js:9-20) reads from a newmtl block.  Textures (map_*) are browser-only
+// in the reference (createImageBitmap, :33-40) and rejected here.
+struct MtlMat {
+    bool ka = false, kd = false, ks = false;
+    float Ka[3] = {0, 0, 0}, Kd[3] = {0, 0, 0}, Ks[3] = {0, 0, 0};
+    double Ns = NAN;  // NaN: absent (`data.Ns || 0`)
+};
+struct MtlLib {
+    std::vector<MtlMat> mats;
+    std::map<std::string, int32_t> by_name;  // ret[name] = ...: a later definition replaces an earlier one
+};
+
+// parseMtlFile (objloader.js:58-123) over the text of every mtllib, in order (loadMtlFiles merges them
+// with Object.assign).
+void parse_mtl(const char *text, size_t n, MtlLib &lib) {
+    std::vector<std::string> t;
+    const char *p = text, *end = text + n;
+    bool have = false;
+    std::string name;
+    MtlMat cur;
+    auto commit = [&]() {
+        if (!have) return;
+        auto it = lib.by_name.find(name);
+        if (it != lib.by_name.end()) lib.mats[it->second] = cur;
+        else {
+            lib.by_name[name] = (int32_t)lib.mats.size();
+            lib.mats.push_back(cur);
+        }
+    };
+    while (p <= end) {
+        const char *e = (const char *)memchr(p, '\n', end - p);
+        if (!e) e = end;
+        tokenize(p, e, t);
+        p = e + 1;
+        if (t.empty() || t[0][0] == '#') continue;  // /^\s*($|#)/
+        const std::string &k = t[0];
+        if (k == "newmtl") {
+            commit();
+            name = t.size() > 1 ? t[1] : "undefined";
+            cur = MtlMat{};
+            have = true;
+            continue;
+        }
+        if (!have) fail("material parameter " + k + " before any newmtl");  // curr is null in the reference
+        auto num = [&](size_t i) { return i < t.size() ? js_parse_float(t[i]) : NAN; };
+        if (k == "Ka" || k == "Kd" || k == "Ks") {  // Vec.of(t[1], t[2], t[3])
+            float *dst = k == "Ka" ? cur.Ka : k == "Kd" ? cur.Kd : cur.Ks;
+            for (int i = 0; i < 3; ++i) dst[i] = f32(num(1 + i));
+            (k == "Ka" ? cur.ka : k == "Kd" ? cur.kd : cur.ks) = true;
+        } else if (k == "Ke" || k == "Tf") {
+            // stored, never read by makeMaterial
+        } else if (k == "Ns" || k == "Ni" || k == "illum" || k == "d" || k == "Tr") {
+            // Ni, illum, d and Tr only reach the discarded Fresnel material (objloader.js:16-18) or nothing
+            if (k == "Ns") {
+                if (t.size() < 2) cur.Ns = NAN;  // curr.Ns = undefined -> smoothness 0
+                else {
+                    cur.Ns = js_parse_float(t[1]);
+                    if (cur.Ns != cur.Ns) fail("non-numeric Ns is not supported: " + t[1]);  // a string smoothness
+                }
+            }
+        } else if (k == "map_Ka" || k == "map_Kd" || k == "map_Ks") {
+            fail("MTL textures (" + k + ") are browser-only in the reference and not supported");
+        } else {
+            fail("Unsupported material parameter: " + k);
+        }
+    }
+    commit();
+}
+
 // parseObjFile (objloader.js:144-221) with loadObjFile's minArea filter (:224-231).
-void parse_obj(const char *text, size_t n, double min_area, const double *prim_transform, std::vector<Tri> &tris) {
+void parse_obj(const char *text, size_t n, double min_area, const double *prim_transform, const MtlLib &mtl,
+               std::vector<Tri> &tris) {
+    int32_t cur_mtl = -1;  // currentMaterial = defaultMaterial
     std::vector<V4> pos, tex, nrm;
     std::vector<std::string> t;
     const char *p = text, *end = text + n;
@@ -212,9 +286,14 @@ void parse_obj(const char *text, size_t n, double min_area, const double *prim_t
         p = e + 1;
         if (t.empty() || t[0][0] == '#') continue;  // /^\s*($|#)/
         const std::string &k = t[0];
-        if (k == "mtllib") continue;
-        if (k == "usemtl")
-            fail("usemtl is not supported by the native OBJ ingest (pass the material on the template primitive)");
+        if (k == "mtllib") continue;  // the caller passes the mtllib texts (loadMtlFiles)
+        if (k == "usemtl") {
+            const std::string nm = t.size() > 1 ? t[1] : "undefined";
+            auto it = mtl.by_name.find(nm);
+            if (it == mtl.by_name.end()) fail("No material defined with name: " + nm);
+            cur_mtl = it->second;
+            continue;
+        }
         if (k == "f") {
             std::vector<Idx> ix;
             for (size_t i = 1; i < t.size(); ++i) ix.push_back(parse_index(t[i]));
@@ -245,6 +324,7 @@ void parse_obj(const char *text, size_t n, double min_area, const double *prim_t
                         for (int d = 0; d < 4; ++d) tr.vn[c][d] = v.v[d];
                     }
                 }
+                tr.mtl = cur_mtl;
                 triangle_ctor(tr);
                 if (tr.area >= min_area) {
                     triangle_bounds(tr, prim_transform);
@@ -521,12 +601,62 @@ std::vector<uint8_t> write_blob(const Sections &S) {
 
 void put4(float *dst, const float *src) { memcpy(dst, src, 16); }
 
+// makeMaterial(data) (objloader.js:9-20) as blob records: the Fresnel / path-tracing material it
+// builds for a finite Ni is never returned (missing `return`), so every MTL material is
+// PhongMaterial(Vec.of(1,1,1), ambient, diffuse, specular, Ns || 0) with ambient / diffuse / specular
+// = Solid(K? given ? K? : Vec.of(0,0,0)) and reflectivity = transmissivity = Scaled(White, 0)
+// (PhongMaterial defaults, materials.js:196-205).  Encoded as jsraytracer_amd/js/scene_blob.js does.
+int32_t mtl_material(Sections &S, const MtlMat &m, int32_t &white) {
+    auto solid = [&](const float *v) {
+        jsrt_rec_mcolor r;
+        memset(&r, 0, sizeof r);
+        r.kind = JSRT_MC_SOLID;
+        r.a = r.b = -1;
+        r.len = 3;
+        for (int i = 0; i < 3; ++i) r.vec[i] = v[i];
+        return append(S, JSRT_SEC_MCOLOR, r);
+    };
+    static const float one[3] = {1, 1, 1}, zero[3] = {0, 0, 0};
+    if (white < 0) white = solid(one);  // SolidMaterialColor.White (shared)
+    auto scaled0 = [&]() {
+        jsrt_rec_mcolor r;
+        memset(&r, 0, sizeof r);
+        r.kind = JSRT_MC_SCALED_SCALAR;
+        r.a = white;
+        r.b = -1;
+        r.scalar = 0.0;
+        return append(S, JSRT_SEC_MCOLOR, r);
+    };
+    jsrt_rec_material M;
+    memset(&M, 0, sizeof M);
+    M.kind = JSRT_MAT_PHONG;
+    M.base = solid(one);
+    M.ambient = solid(m.ka ? m.Ka : zero);
+    M.diffuse = solid(m.kd ? m.Kd : zero);
+    M.specular = solid(m.ks ? m.Ks : zero);
+    M.reflect = scaled0();
+    M.transmit = scaled0();
+    M.color = -1;
+    M.smoothness = (m.Ns != m.Ns || m.Ns == 0) ? 0.0 : m.Ns;  // data.Ns || 0
+    M.ratio = 1;
+    M.mirror_prob = 0;
+    M.opacity = 0;
+    return append(S, JSRT_SEC_MATERIAL, M);
+}
+
 void splice(const void *blob, size_t n, const jsrt_mesh_options *opt, const char *obj, size_t obj_len,
-            std::vector<uint8_t> &out, jsrt_mesh_info *info) {
+            const char *mtl_text, size_t mtl_len, std::vector<uint8_t> &out, jsrt_mesh_info *info) {
     Sections S = read_blob(blob, n);
+    MtlLib mtl;
+    for (size_t a = 0; a < mtl_len;) {  // one parseMtlFile per NUL-separated file, merged like Object.assign
+        const char *z = (const char *)memchr(mtl_text + a, 0, mtl_len - a);
+        const size_t b = z ? (size_t)(z - mtl_text) : mtl_len;
+        parse_mtl(mtl_text + a, b - a, mtl);
+        a = b + 1;
+    }
     uint32_t n_obj, n_bvh, n_chld, n_geom, n_tri, n_mats;
     for (uint32_t tag : {JSRT_SEC_GEOMETRY, JSRT_SEC_OBJECT, JSRT_SEC_CHILD, JSRT_SEC_BVHNODE, JSRT_SEC_TRIANGLE,
-                         JSRT_SEC_MATRIX})
+                         JSRT_SEC_MATRIX, JSRT_SEC_MCOLOR, JSRT_SEC_MATERIAL})
         if (S.find(tag) < 0) (void)recs<uint8_t>(S, tag, n_obj);  // create missing (empty) sections
     const jsrt_rec_object *O = recs<jsrt_rec_object>(S, JSRT_SEC_OBJECT, n_obj);
     const jsrt_rec_bvhnode *N = recs<jsrt_rec_bvhnode>(S, JSRT_SEC_BVHNODE, n_bvh);
@@ -556,7 +686,7 @@ void splice(const void *blob, size_t n, const jsrt_mesh_options *opt, const char
 
     std::vector<Tri> tris;
     const double min_area = opt ? opt->min_area : 0.00001;
-    parse_obj(obj, obj_len, min_area, pm, tris);
+    parse_obj(obj, obj_len, min_area, pm, mtl, tris);
     if (tris.empty()) fail("the OBJ text holds no triangle of at least min_area", -1);
 
     Builder B(tris);
@@ -565,7 +695,8 @@ void splice(const void *blob, size_t n, const jsrt_mesh_options *opt, const char
     B.build(std::move(all), 0);
 
     // records: geometry + triangle + primitive per triangle, nodes in pre-order
-    std::vector<int32_t> prim_of(tris.size());
+    std::vector<int32_t> prim_of(tris.size()), mat_of(mtl.mats.size(), -1);
+    int32_t white = -1;
     for (size_t i = 0; i < tris.size(); ++i) {
         const Tri &t = tris[i];
         jsrt_rec_triangle tr;
@@ -593,6 +724,10 @@ void splice(const void *blob, size_t n, const jsrt_mesh_options *opt, const char
         g.index = append(S, JSRT_SEC_TRIANGLE, tr);
         jsrt_rec_object o = tmpl;
         o.geometry = append(S, JSRT_SEC_GEOMETRY, g);
+        if (t.mtl >= 0) {  // usemtl: the MTL material (one record per material used)
+            if (mat_of[t.mtl] < 0) mat_of[t.mtl] = mtl_material(S, mtl.mats[t.mtl], white);
+            o.material = mat_of[t.mtl];
+        }
         prim_of[i] = append(S, JSRT_SEC_OBJECT, o);
     }
     uint32_t base;
@@ -624,7 +759,11 @@ void splice(const void *blob, size_t n, const jsrt_mesh_options *opt, const char
         }
         append(S, JSRT_SEC_BVHNODE, rec);
     }
-    recs<jsrt_rec_object>(S, JSRT_SEC_OBJECT, n_obj)[bo].bvh_root = (int32_t)base;  // old template tree is now unreferenced
+    // every BVHAggregate over the template tree gets the new one: `new BVHAggregate(objs, tie1.kdtree, T)`
+    // instances share a tree (tests/starwars/test.mjs); the old template tree is now unreferenced
+    jsrt_rec_object *Ow = recs<jsrt_rec_object>(S, JSRT_SEC_OBJECT, n_obj);
+    for (uint32_t i = 0; i < n_obj; ++i)
+        if (Ow[i].kind == JSRT_OBJ_BVH && Ow[i].bvh_root == r) Ow[i].bvh_root = (int32_t)base;
     out = write_blob(S);
     if (info) {
         memset(info, 0, sizeof *info);
@@ -641,13 +780,20 @@ extern "C" {
 
 int jsrt_blob_attach_obj(const void *blob, size_t n, const char *obj_text, size_t obj_len,
                          const jsrt_mesh_options *options, void **out_blob, size_t *out_n, jsrt_mesh_info *info) {
+    return jsrt_blob_attach_obj_mtl(blob, n, obj_text, obj_len, nullptr, 0, options, out_blob, out_n, info);
+}
+
+int jsrt_blob_attach_obj_mtl(const void *blob, size_t n, const char *obj_text, size_t obj_len, const char *mtl_text,
+                             size_t mtl_len, const jsrt_mesh_options *options, void **out_blob, size_t *out_n,
+                             jsrt_mesh_info *info) {
     if (!out_blob || !out_n) return jsrt::record_error(-1, "out_blob / out_n is NULL");
     *out_blob = nullptr;
     *out_n = 0;
     if (!obj_text && obj_len) return jsrt::record_error(-1, "obj_text is NULL");
     try {
         std::vector<uint8_t> out;
-        splice(blob, n, options, obj_text ? obj_text : "", obj_len, out, info);
+        if (!mtl_text && mtl_len) return jsrt::record_error(-1, "mtl_text is NULL");
+        splice(blob, n, options, obj_text ? obj_text : "", obj_len, mtl_text, mtl_len, out, info);
         void *p = malloc(out.size());
         if (!p) return jsrt::record_error(-4, "out of host memory");
         memcpy(p, out.data(), out.size());

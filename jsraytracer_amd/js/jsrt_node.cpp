@@ -330,6 +330,22 @@ napi_value Render(napi_env env, napi_callback_info info) {
 
 // attachObj(blob, objText, {bvhObject, minArea}?) -> {blob: Buffer, triangles, nodes, maxDepth}
 // loadObjFile + BVHAggregate.build natively (include/jsrt_mesh.h; objloader.js:224-231, aggregates.js:33-41)
+// string (UTF-8) or Uint8Array/Buffer contents
+bool get_text(napi_env env, napi_value v, std::string &out) {
+    void *b = nullptr;
+    size_t l = 0;
+    if (get_bytes(env, v, &b, &l)) {
+        out.assign((const char *)b, l);
+        return true;
+    }
+    size_t n = 0;
+    if (napi_get_value_string_utf8(env, v, nullptr, 0, &n) != napi_ok) return false;
+    out.resize(n + 1);
+    napi_get_value_string_utf8(env, v, &out[0], n + 1, &n);
+    out.resize(n);
+    return true;
+}
+
 napi_value AttachObj(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3];
@@ -340,20 +356,10 @@ napi_value AttachObj(napi_env env, napi_callback_info info) {
         napi_throw_type_error(env, "JSRT", "attachObj(blob: Uint8Array, objText: string | Uint8Array, opts?)");
         return nullptr;
     }
-    std::string text;
-    void *tb = nullptr;
-    size_t tl = 0;
-    if (get_bytes(env, argv[1], &tb, &tl)) {
-        text.assign((const char *)tb, tl);
-    } else {
-        size_t n = 0;
-        if (napi_get_value_string_utf8(env, argv[1], nullptr, 0, &n) != napi_ok) {
-            napi_throw_type_error(env, "JSRT", "attachObj: objText must be a string or Uint8Array");
-            return nullptr;
-        }
-        text.resize(n + 1);
-        napi_get_value_string_utf8(env, argv[1], &text[0], n + 1, &n);
-        text.resize(n);
+    std::string text, mtl;
+    if (!get_text(env, argv[1], text)) {
+        napi_throw_type_error(env, "JSRT", "attachObj: objText must be a string or Uint8Array");
+        return nullptr;
     }
     jsrt_mesh_options opt{-1, 0, 0.00001};
     if (argc > 2) {
@@ -368,12 +374,32 @@ napi_value AttachObj(napi_env env, napi_callback_info info) {
             if (napi_has_named_property(env, argv[2], "minArea", &has) == napi_ok && has &&
                 napi_get_named_property(env, argv[2], "minArea", &v) == napi_ok)
                 napi_get_value_double(env, v, &opt.min_area);
+            // mtl: the mtllib files' texts (string | Uint8Array, or an array of them in mtllib order)
+            if (napi_has_named_property(env, argv[2], "mtl", &has) == napi_ok && has &&
+                napi_get_named_property(env, argv[2], "mtl", &v) == napi_ok) {
+                bool arr = false;
+                napi_is_array(env, v, &arr);
+                uint32_t n = 1;
+                if (arr) napi_get_array_length(env, v, &n);
+                for (uint32_t i = 0; i < n; ++i) {
+                    napi_value e = v;
+                    if (arr) napi_get_element(env, v, i, &e);
+                    std::string one;
+                    if (!get_text(env, e, one)) {
+                        napi_throw_type_error(env, "JSRT", "attachObj: opts.mtl must hold strings or Uint8Arrays");
+                        return nullptr;
+                    }
+                    if (i) mtl.push_back('\0');
+                    mtl += one;
+                }
+            }
         }
     }
     void *out = nullptr;
     size_t out_n = 0;
     jsrt_mesh_info mi;
-    if (jsrt_blob_attach_obj(data, len, text.data(), text.size(), &opt, &out, &out_n, &mi) != 0)
+    if (jsrt_blob_attach_obj_mtl(data, len, text.data(), text.size(), mtl.data(), mtl.size(), &opt, &out, &out_n,
+                                 &mi) != 0)
         return throw_jsrt(env, "jsrt_blob_attach_obj");
     napi_value buf, o, v;
     void *dst = nullptr;

@@ -82,7 +82,7 @@ class SceneBlobWriter {
     constructor() {
         this.sec = {};
         for (const t of Object.keys(REC_SIZE)) this.sec[t] = [];
-        this.maps = { mc: new Map(), mat: new Map(), geom: new Map(), obj: new Map(), matrix: new Map(),
+        this.maps = { mc: new Map(), mat: new Map(), geom: new Map(), obj: new Map(), bvh: new Map(), matrix: new Map(),
                       matrixBytes: new Map(), sdf: new Map(), sdfgeom: new Map() };
     }
     push(tag, rec) { this.sec[tag].push(rec); return this.sec[tag].length - 1; }
@@ -254,8 +254,11 @@ class SceneBlobWriter {
     }
 
     bvhIndex(node) {
+        // `new BVHAggregate(objs, other.kdtree, T)` instances share one tree (tests/starwars/test.mjs)
+        if (this.maps.bvh.has(node)) return this.maps.bvh.get(node);
         const r = new Rec(64);
         const idx = this.push("BVHN", r);
+        this.maps.bvh.set(node, idx);
         r.vec(0, assertVec(node.aabb.center, "BVH aabb")).vec(16, assertVec(node.aabb.half_size, "BVH aabb"));
         r.u32(32, node.isLeaf ? 1 : 0).i32(36, -1).i32(40, -1).i32(44, 0).i32(48, 0).i32(52, node.depth);
         if (node.isLeaf) {

@@ -115,3 +115,36 @@ def golden_image(tag, width, height):
 def golden_kats():
     with open(os.path.join(GOLDEN, "kats.json")) as f:
         return json.load(f)
+
+
+# ---- mesh fixtures (oracle/refharness/regen_mesh_fixtures.sh): skeleton + OBJ + MTL per scene ----
+MESHES = os.path.join(GOLDEN, "meshes")
+
+
+def mesh_topology():
+    with open(os.path.join(MESHES, "topology.json")) as f:
+        return json.load(f)
+
+
+def mesh_index():
+    with open(os.path.join(MESHES, "index.json")) as f:
+        return json.load(f)["renders"]
+
+
+def mesh_scene(name, jr=None):
+    """(blob, [info per tree]) of a mesh scene: its reference-exported skeleton with every OBJ (and its
+    mtllib files) attached by the native ingest (include/jsrt_mesh.h), one BVHAggregate.build each, in
+    the reference's call order.  The trees are pinned to the reference's by tests/test_mesh_build.py."""
+    if jr is None:
+        import jsraytracer_amd as jr
+    topo = mesh_topology()[name]
+
+    def read(f):
+        with gzip.open(os.path.join(MESHES, f), "rb") as g:
+            return g.read()
+    blob, infos = read(topo["skeleton"]), []
+    for t in topo["trees"]:
+        blob, info = jr.attach_obj(blob, read(t["obj_fixture"]), bvh_object=t["bvh_object"],
+                                   mtl_texts=[read(m) for m in t["mtl_fixtures"]])
+        infos.append(info)
+    return blob, infos

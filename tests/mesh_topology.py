@@ -4,15 +4,18 @@ The digest walks the tree the way the reference's exporter and traversal see it 
 subtree first, aggregates.js:65-87,221-222) and hashes, per node: depth, leaf flag, AABB centre and
 half size (f32 bit patterns); per leaf object: the Triangle record fields the reference computes
 (geometry.js:335-354: ps, v0, v1, normal, delta, d00, d11, d01, denom, area, vertex normals, UVs),
-the material index and the shadow flag.  Two blobs with equal digests hold bit-identical trees, so
-closest-hit ties break alike.  Record indices (which differ between exporters) are not hashed.
+the material (its MATL record with every MaterialColor index replaced by that MCOL record's own
+content key, recursively: makeMaterial's PhongMaterial from an MTL file, objloader.js:9-20) and the
+shadow flag.  Two blobs with equal digests hold bit-identical trees with equal materials, so
+closest-hit ties break alike and shading agrees.  Record indices (which differ between exporters) are
+not hashed.
 """
 import hashlib
 import struct
 
 import numpy as np
 
-TAGS = {"OBJS": 32, "BVHN": 64, "TRIS": 256, "GEOM": 48, "CHLD": 4, "MATS": 256}
+TAGS = {"OBJS": 32, "BVHN": 64, "TRIS": 256, "GEOM": 48, "CHLD": 4, "MATS": 256, "MCOL": 40, "MATL": 64}
 
 
 def fourcc(s):
@@ -41,6 +44,32 @@ def bvh_objects(blob):
     return [i for i in range(len(o)) if o[i, 0] == 3]
 
 
+class _Materials:
+    """Content keys of MATL / MCOL records (record indices replaced by the referenced content)."""
+
+    def __init__(self, sec):
+        self.mcol, self.matl = sec["MCOL"][1], sec["MATL"][1]
+        self.kc, self.km = {}, {}
+
+    def mc(self, i):
+        if i < 0:
+            return b"-"
+        if i not in self.kc:
+            r = self.mcol[40 * i:40 * i + 40]
+            kind, a, b = struct.unpack_from("<I2i", r, 0)
+            self.kc[i] = hashlib.sha256(struct.pack("<I", kind) + self.mc(a) + self.mc(b) + r[12:]).digest()
+        return self.kc[i]
+
+    def mat(self, i):
+        if i < 0:
+            return b"-"
+        if i not in self.km:
+            r = self.matl[64 * i:64 * i + 64]
+            kind, *refs = struct.unpack_from("<I7i", r, 0)
+            self.km[i] = hashlib.sha256(struct.pack("<I", kind) + b"".join(self.mc(x) for x in refs) + r[32:]).digest()
+        return self.km[i]
+
+
 def digest(blob, bvh_object=None):
     """(sha256 hex, nodes, max_depth, triangles) of a BVHAggregate's tree."""
     sec = sections(blob)
@@ -51,6 +80,7 @@ def digest(blob, bvh_object=None):
     C = np.frombuffer(sec["CHLD"][1], np.int32)
     G = np.frombuffer(sec["GEOM"][1], np.int32).reshape(-1, 12)
     T = sec["TRIS"][1]
+    M = _Materials(sec)
     h = hashlib.sha256()
     nodes = tris = maxd = 0
     stack = [int(O[bvh_object, 6])]
@@ -67,7 +97,7 @@ def digest(blob, bvh_object=None):
                 kind, geom, mat, casts = (int(x) for x in O[c, :4])
                 assert kind == 1 and G[geom, 0] == 7, "BVH leaf object is not a Primitive over a Triangle"
                 t = int(G[geom, 1])
-                h.update(struct.pack("<iI", mat, casts) + T[256 * t:256 * t + 256])
+                h.update(M.mat(mat) + struct.pack("<I", casts) + T[256 * t:256 * t + 256])
                 tris += 1
         else:
             stack.append(greater)  # pre-order, lesser first

@@ -10,8 +10,6 @@ and compared: RGBA8 bit-exact, f32 colour |d| <= 1e-5 (north_star), same non-fin
 A second render of the same frame through the multi-GPU tile layout (jsrt_render_device, 16-column
 blocks dealt to 2 "ranks" on device 0) must composite to the same bytes.
 """
-import gzip
-import json
 import os
 
 import numpy as np
@@ -21,7 +19,6 @@ from oracle import pyoracle
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MESHES = os.path.join(ROOT, "tests", "golden", "meshes")
 TOL = 1e-5
 
 # (config, scene, W, H, spp, depth, column stride): bench.py CONFIGS at full size
@@ -36,12 +33,7 @@ CASES = [
 def _blob(scene):
     if scene != "dragon":
         return pyoracle.golden_scene(scene)
-    import jsraytracer_amd as jr
-    topo = json.load(open(os.path.join(MESHES, "topology.json")))[scene]
-    with gzip.open(os.path.join(MESHES, topo["skeleton"]), "rb") as f:
-        skel = f.read()
-    blob, _ = jr.load_obj_scene(skel, os.path.join(MESHES, topo["obj_fixture"]))
-    return blob
+    return pyoracle.mesh_scene(scene)[0]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])

@@ -72,6 +72,24 @@ def test_addon_attach_obj_matches_python_and_reference(addon, tmp_path):
     assert mt.digest(py) == mt.digest(pyoracle.golden_scene("bunny"))
 
 
+def test_addon_attach_obj_with_mtl_matches_python(addon, tmp_path):
+    """attachObj(skel, obj, {mtl: [text...], bvhObject}) -- the x-wing with its mtllib (usemtl on every
+    face) -- gives the Python binding's bytes."""
+    from oracle import pyoracle
+    meshes = os.path.join(ROOT, "tests", "golden", "meshes")
+    t = pyoracle.mesh_topology()["x-wing"]
+    out = tmp_path / "xwing.jsrt"
+    rd = "(f)=>z.gunzipSync(fs.readFileSync(" + json.dumps(meshes) + "+'/'+f))"
+    code = (f"const a=require({json.dumps(addon)}); const z=require('zlib'), fs=require('fs'); const rd={rd};"
+            f"const r=a.attachObj(rd({json.dumps(t['skeleton'])}), rd({json.dumps(t['obj_fixture'])}),"
+            f"{{bvhObject:{t['bvh_object']}, mtl:[rd({json.dumps(t['mtl_fixtures'][0])}).toString()]}});"
+            f"fs.writeFileSync({json.dumps(str(out))}, r.blob); console.log(r.triangles, r.nodes);")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == [str(t["triangles"]), str(t["nodes"])]
+    assert out.read_bytes() == pyoracle.mesh_scene("x-wing")[0]
+
+
 def test_addon_errors_are_thrown(addon):
     r = _node(f"const a=require({json.dumps(addon)});"
               "try {{ a.sceneCreate(new Uint8Array(10)); console.log('no throw'); }} catch (e) {{ console.log(e.message); }}"
