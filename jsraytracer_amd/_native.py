@@ -48,10 +48,17 @@ EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_rende
            "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
+# exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
+JSON_EXPORTS = ["jsrt_blob_from_json"]
 
 
 class MeshOptions(ctypes.Structure):
     _fields_ = [("bvh_object", ctypes.c_int32), ("pad", ctypes.c_int32), ("min_area", ctypes.c_double)]
+
+
+class JsonInfo(ctypes.Structure):
+    _fields_ = [("objects", ctypes.c_int64), ("triangles", ctypes.c_int64), ("bvh_nodes", ctypes.c_int64),
+                ("psdata_matched", ctypes.c_int64)]
 
 
 class MeshInfo(ctypes.Structure):
@@ -100,6 +107,10 @@ def lib():
                                            ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(MeshOptions),
                                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
                                            ctypes.POINTER(MeshInfo)]
+    L.jsrt_blob_from_json.restype = ctypes.c_int
+    L.jsrt_blob_from_json.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(JsonInfo)]
     L.jsrt_blob_free.restype = None
     L.jsrt_blob_free.argtypes = [ctypes.c_void_p]
     _lib = L

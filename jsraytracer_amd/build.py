@@ -24,14 +24,15 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-f
          "-Wall", "-Wno-unused-function"]
 
 INCLUDE = os.path.join(HERE, "..", "include")
-PUBLIC = ["jsrt.h", "jsrt_scene.h", "jsrt_mesh.h"]
+PUBLIC = ["jsrt.h", "jsrt_scene.h", "jsrt_mesh.h", "jsrt_json.h"]
 # objects: (object stem, source, extra defines, dependencies); an object is rebuilt only when these change
 UNITS = [("render", "render.hip", [], HEADERS + ["jsrt.h", "jsrt_scene.h"])]
 UNITS += [(f"render_pf{pf}", "render_pf.hip", [f"-DJSRT_PF={pf}"], HEADERS + ["jsrt.h", "jsrt_scene.h"])
           for pf in PROFILES.values()]
 UNITS += [("capi", "capi.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
           ("scene_load", "scene_load.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
-          ("mesh_build", "mesh_build.cpp", [], ["jsrt_mesh.h", "jsrt_scene.h"])]
+          ("mesh_build", "mesh_build.cpp", [], ["jsrt_mesh.h", "jsrt_scene.h", "obj_parse.h"]),
+          ("json_scene", "json_scene.cpp", [], ["jsrt_json.h", "jsrt_scene.h", "obj_parse.h"])]
 OBJ_FLAGS = [f for f in FLAGS if f != "-shared"]
 
 
@@ -62,14 +63,22 @@ def _stale():
 def build(force=False, verbose=False, variant=None, defines=(), profiles=None):
     """variant: build _build/libjsrt_<variant>.so with extra -D defines (A/B experiments).  profiles:
     for a variant, the kernel profiles (PF numbers) recompiled with the defines; the other objects are
-    the default build's (fast A/B of one scene class)."""
+    the default build's (fast A/B of one scene class).  Concurrent callers (pytest-xdist workers) are
+    serialised on a lock file, so a stale library is rebuilt once."""
     os.makedirs(OUT, exist_ok=True)
+    import fcntl
+    with open(os.path.join(OUT, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return _build_locked(force, verbose, variant, defines, profiles)
+
+
+def _build_locked(force, verbose, variant, defines, profiles):
     lib = LIB if variant is None else os.path.join(OUT, f"libjsrt_{variant}.so")
     tag = "" if variant is None else f"_{variant}"
     if variant is None and not force and not _stale():
         return LIB
     if variant is not None:
-        build(verbose=verbose)  # the default objects a partial variant links against
+        _build_locked(False, verbose, None, (), None)  # the default objects a partial variant links against
     jobs, objs = [], []
     for stem, src, defs, deps in UNITS:
         mine = variant is not None and (profiles is None or any(stem == f"render_pf{p}" for p in profiles))

@@ -23,18 +23,14 @@
 
 #include "../../include/jsrt_mesh.h"
 #include "../../include/jsrt_scene.h"
+#include "obj_parse.h"
 
 namespace jsrt {
 int record_error(int code, const std::string &m);  // capi.cpp (jsrt_last_error)
 }
 
 namespace {
-
-struct Fail {
-    int code;
-    std::string msg;
-};
-[[noreturn]] void fail(const std::string &m, int code = -2) { throw Fail{code, m}; }
+using namespace jsrt::objp;
 
 // ---------------------------------------------------------------- JS number parsing / Vec helpers
 inline bool js_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
@@ -83,19 +79,10 @@ struct V4 {
 };
 
 // ---------------------------------------------------------------- OBJ text -> triangles
-struct Tri {
-    int32_t mtl = -1;  // MTL material (index into the parsed list) or -1: loadObjFile's defaultMaterial
-    float ps[3][4];
-    int has_normal = 0, has_uv = 0, uv_len = 0;
-    float vn[3][4] = {}, uv[3][4] = {};
-    // Triangle constructor results (geometry.js:335-354)
-    float v0[4], v1[4], normal[4];
-    double delta, d00, d11, d01, denom, area;
-    // Primitive.getBoundingBox (world.js:138-140 -> geometry.js:378-380 -> AABB.fromPoints)
-    float bmin[4], bmax[4], bcenter[4];
-};
+}  // namespace
 
-// Triangle constructor (geometry.js:335-354) in the reference's numeric model.
+namespace jsrt {
+namespace objp {
 void triangle_ctor(Tri &t) {
     float a[3], b[3];
     for (int i = 0; i < 3; ++i) {  // ps[k].minus(ps[0]) is an f32 op per component, then to3()
@@ -130,6 +117,10 @@ void triangle_ctor(Tri &t) {
     t.d01 = (double)a[0] * b[0] + (double)a[1] * b[1] + (double)a[2] * b[2];
     t.denom = t.d00 * t.d11 - t.d01 * t.d01;
 }
+}  // namespace objp
+}  // namespace jsrt
+
+namespace {
 
 // AABB.fromMinMax centre (math.js:233-235 mix(b, 0.5)) for finite boxes
 inline float mid(float lo, float hi) { return f32((1 - 0.5) * lo + 0.5 * (double)hi); }
@@ -204,16 +195,11 @@ const T &at_index(const std::vector<T> &v, double i, const char *what) {
 // ---------------------------------------------------------------- MTL (objloader.js:58-123)
 // What makeMaterial (objloader.js:9-20) reads from a newmtl block.  Textures (map_*) are browser-only
 // in the reference (createImageBitmap, :33-40) and rejected here.
-struct MtlMat {
-    bool ka = false, kd = false, ks = false;
-    float Ka[3] = {0, 0, 0}, Kd[3] = {0, 0, 0}, Ks[3] = {0, 0, 0};
-    double Ns = NAN;  // NaN: absent (`data.Ns || 0`)
-};
-struct MtlLib {
-    std::vector<MtlMat> mats;
-    std::map<std::string, int32_t> by_name;  // ret[name] = ...: a later definition replaces an earlier one
-};
 
+}  // namespace
+
+namespace jsrt {
+namespace objp {
 // parseMtlFile (objloader.js:58-123) over the text of every mtllib, in order (loadMtlFiles merges them
 // with Object.assign).
 void parse_mtl(const char *text, size_t n, MtlLib &lib) {
@@ -349,6 +335,10 @@ void parse_obj(const char *text, size_t n, double min_area, const double *prim_t
             fail("Error while attempting to parse obj file on line \"" + std::string(line, e) + "\"");
     }
 }
+}  // namespace objp
+}  // namespace jsrt
+
+namespace {
 
 // ---------------------------------------------------------------- BVH build (aggregates.js:65-185)
 struct Box {  // only min/max are state; centre/half are derived as AABB.fromMinMax does

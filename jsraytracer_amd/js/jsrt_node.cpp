@@ -22,6 +22,7 @@
 #include <string>
 
 #include "../../include/jsrt.h"
+#include "../../include/jsrt_json.h"
 #include "../../include/jsrt_mesh.h"
 
 namespace {
@@ -417,6 +418,63 @@ napi_value AttachObj(napi_env env, napi_callback_info info) {
     return o;
 }
 
+// blobFromJson(jsonText, {psdataObj}?) -> {blob: Buffer, objects, triangles, psdataMatched}
+// Serializer.deserializeJSON (serializer.js:69-71) for the dragon_json-style flow, natively
+// (include/jsrt_json.h); psdataObj: the OBJ text(s) the meshes came from (vertex normals / UVs).
+napi_value BlobFromJson(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    std::string text, side;
+    if (argc < 1 || !get_text(env, argv[0], text)) {
+        napi_throw_type_error(env, "JSRT", "blobFromJson(jsonText: string | Uint8Array, opts?)");
+        return nullptr;
+    }
+    if (argc > 1) {
+        napi_valuetype t;
+        napi_typeof(env, argv[1], &t);
+        napi_value v;
+        bool has = false;
+        if (t == napi_object && napi_has_named_property(env, argv[1], "psdataObj", &has) == napi_ok && has &&
+            napi_get_named_property(env, argv[1], "psdataObj", &v) == napi_ok) {
+            bool arr = false;
+            napi_is_array(env, v, &arr);
+            uint32_t n = 1;
+            if (arr) napi_get_array_length(env, v, &n);
+            for (uint32_t i = 0; i < n; ++i) {
+                napi_value e = v;
+                if (arr) napi_get_element(env, v, i, &e);
+                std::string one;
+                if (!get_text(env, e, one)) {
+                    napi_throw_type_error(env, "JSRT", "blobFromJson: opts.psdataObj must hold strings or Uint8Arrays");
+                    return nullptr;
+                }
+                if (i) side.push_back('\0');
+                side += one;
+            }
+        }
+    }
+    void *out = nullptr;
+    size_t out_n = 0;
+    jsrt_json_info ji;
+    if (jsrt_blob_from_json(text.data(), text.size(), side.data(), side.size(), &out, &out_n, &ji) != 0)
+        return throw_jsrt(env, "jsrt_blob_from_json");
+    napi_value buf, o, v;
+    void *dst = nullptr;
+    napi_status st = napi_create_buffer_copy(env, out_n, out, &dst, &buf);
+    jsrt_blob_free(out);
+    NAPI_OK(st);
+    NAPI_OK(napi_create_object(env, &o));
+    napi_set_named_property(env, o, "blob", buf);
+    napi_create_double(env, (double)ji.objects, &v);
+    napi_set_named_property(env, o, "objects", v);
+    napi_create_double(env, (double)ji.triangles, &v);
+    napi_set_named_property(env, o, "triangles", v);
+    napi_create_double(env, (double)ji.psdata_matched, &v);
+    napi_set_named_property(env, o, "psdataMatched", v);
+    return o;
+}
+
 napi_value DeviceCount(napi_env env, napi_callback_info) {
     napi_value v;
     napi_create_int32(env, jsrt_device_count(), &v);
@@ -450,6 +508,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"abiVersion", nullptr, AbiVersion, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"ownedColumns", nullptr, OwnedColumns, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"attachObj", nullptr, AttachObj, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"blobFromJson", nullptr, BlobFromJson, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

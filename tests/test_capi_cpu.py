@@ -30,7 +30,9 @@ def test_header_symbols_exported(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
     mesh = _declared("jsrt_mesh.h")
     assert set(mesh) == set(_native.MESH_EXPORTS)
-    for sym in declared + mesh:
+    js = _declared("jsrt_json.h")
+    assert set(js) == set(_native.JSON_EXPORTS)
+    for sym in declared + mesh + js:
         assert re.search(rf"\bT {sym}$", out, re.M), f"{sym} not exported"
         assert hasattr(lib, sym)
 

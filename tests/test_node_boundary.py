@@ -42,7 +42,7 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     keys, nums = r.stdout.strip().split("\n")
     assert json.loads(keys) == sorted(["sceneCreate", "sceneDestroy", "renderSync", "render", "deviceCount",
-                                       "abiVersion", "ownedColumns", "attachObj"])
+                                       "abiVersion", "ownedColumns", "attachObj", "blobFromJson"])
     assert nums.split() == ["2", "16", "3"]
 
 
@@ -88,6 +88,25 @@ def test_addon_attach_obj_with_mtl_matches_python(addon, tmp_path):
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == [str(t["triangles"]), str(t["nodes"])]
     assert out.read_bytes() == pyoracle.mesh_scene("x-wing")[0]
+
+
+def test_addon_blob_from_json_matches_reference_export(addon, tmp_path):
+    """blobFromJson (a dragon_json-style test.json, natively) from node: the bunny's Serializer JSON with
+    its OBJ as psdata side-channel gives the golden blob the live exporter wrote."""
+    jdir = os.path.join(ROOT, "tests", "golden", "json")
+    obj = os.path.join(ROOT, "tests", "golden", "meshes", "bunny2.obj.gz")
+    out = tmp_path / "bunny.jsrt"
+    code = (f"const a=require({json.dumps(addon)}); const z=require('zlib'), fs=require('fs');"
+            f"const j=z.gunzipSync(fs.readFileSync({json.dumps(os.path.join(jdir, 'bunny.json.gz'))})).toString();"
+            f"const r=a.blobFromJson(j, {{psdataObj: [z.gunzipSync(fs.readFileSync({json.dumps(obj)}))]}});"
+            f"fs.writeFileSync({json.dumps(str(out))}, r.blob); console.log(r.triangles, r.psdataMatched);"
+            "try { a.blobFromJson('{\"_r\":3}'); console.log('no throw'); } catch (e) { console.log(e.message); }")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert lines[0].split() == ["4968", "4968"]
+    assert lines[1].startswith("jsrt_blob_from_json: ")
+    assert out.read_bytes() == pyoracle.golden_scene("bunny")
 
 
 def test_addon_errors_are_thrown(addon):
