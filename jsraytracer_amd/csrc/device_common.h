@@ -15,6 +15,9 @@
 #include "device_scene.h"
 #include "js_number.h"
 
+// building blocks also compiled for the host (tests/native: filter-vs-exact checks on the CPU)
+#define JSRT_HD __host__ __device__ __forceinline__
+
 namespace jsrt {
 
 #define JS_PI 3.141592653589793
@@ -22,18 +25,18 @@ namespace jsrt {
 
 // --------------------------------------------------------------------------------------------
 // JS scalar semantics
-__device__ __forceinline__ bool is_nan(double x) { return x != x; }
-__device__ __forceinline__ double js_max(double a, double b) {  // Math.max
+JSRT_HD bool is_nan(double x) { return x != x; }
+JSRT_HD double js_max(double a, double b) {  // Math.max
     if (is_nan(a) || is_nan(b)) return __builtin_nan("");
     if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) && __builtin_signbit(b)) ? -0.0 : 0.0;
     return a > b ? a : b;
 }
-__device__ __forceinline__ double js_min(double a, double b) {  // Math.min
+JSRT_HD double js_min(double a, double b) {  // Math.min
     if (is_nan(a) || is_nan(b)) return __builtin_nan("");
     if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) || __builtin_signbit(b)) ? -0.0 : 0.0;
     return a < b ? a : b;
 }
-__device__ __forceinline__ double js_sign(double x) {
+JSRT_HD double js_sign(double x) {
     if (is_nan(x) || x == 0.0) return x;
     return x > 0 ? 1.0 : -1.0;
 }
@@ -52,7 +55,7 @@ __device__ __forceinline__ double js_round(double x) {  // Math.round (half towa
     if (x - r >= 0.5) r += 1.0;
     return r;
 }
-__device__ __forceinline__ float or0(float x) { return (x != x || x == 0.0f) ? 0.0f : x; }  // `x || 0`
+JSRT_HD float or0(float x) { return (x != x || x == 0.0f) ? 0.0f : x; }  // `x || 0`
 
 // --------------------------------------------------------------------------------------------
 // keyed RNG (oracle/refharness/keyed_rng.js)
@@ -80,40 +83,40 @@ struct Rng {
 struct F3 {
     float x, y, z;
 };
-__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
-__device__ __forceinline__ F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ F3 mul(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ F3 scale(F3 a, double s) {  // Vec.times(scalar): f32(x * s) in f64
+JSRT_HD F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+JSRT_HD F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+JSRT_HD F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+JSRT_HD F3 mul(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+JSRT_HD F3 scale(F3 a, double s) {  // Vec.times(scalar): f32(x * s) in f64
     return f3((float)((double)a.x * s), (float)((double)a.y * s), (float)((double)a.z * s));
 }
-__device__ __forceinline__ F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }  // times(-1) is exact
-__device__ __forceinline__ double dot3(F3 a, F3 b) {
+JSRT_HD F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }  // times(-1) is exact
+JSRT_HD double dot3(F3 a, F3 b) {
     return (double)a.x * (double)b.x + (double)a.y * (double)b.y + (double)a.z * (double)b.z;
 }
 // normalized() of a Vec whose 4th component is (+/-)0 or absent: the 4th term only adds a zero
-__device__ __forceinline__ F3 normalized(F3 a) {
+JSRT_HD F3 normalized(F3 a) {
     const double n = sqrt(dot3(a, a));
     return (n > 0.00001) ? scale(a, 1 / n) : a;
 }
-__device__ __forceinline__ double average3(F3 a) {  // Vec.average (math.js:261-266)
+JSRT_HD double average3(F3 a) {  // Vec.average (math.js:261-266)
     return ((((0.0 + (double)a.x) + (double)a.y) + (double)a.z)) / 3;
 }
 
 // Mat(3x4 rows, implicit row 3 = 0,0,0,1) * Vec (math.js:392-397): f64 dot in order, f32 store.
 template <class T>
-__device__ __forceinline__ F3 xf_point(const T *m, F3 o) {  // w = 1 (T: double in any address space)
+JSRT_HD F3 xf_point(const T *m, F3 o) {  // w = 1 (T: double in any address space)
     return f3((float)((((double)o.x * m[0] + (double)o.y * m[1]) + (double)o.z * m[2]) + m[3]),
               (float)((((double)o.x * m[4] + (double)o.y * m[5]) + (double)o.z * m[6]) + m[7]),
               (float)((((double)o.x * m[8] + (double)o.y * m[9]) + (double)o.z * m[10]) + m[11]));
 }
-__device__ __forceinline__ F3 xf_dir(const double *m, F3 d) {  // w = 0: the 4th term only adds a zero
+JSRT_HD F3 xf_dir(const double *m, F3 d) {  // w = 0: the 4th term only adds a zero
     return f3((float)(((double)d.x * m[0] + (double)d.y * m[1]) + (double)d.z * m[2]),
               (float)(((double)d.x * m[4] + (double)d.y * m[5]) + (double)d.z * m[6]),
               (float)(((double)d.x * m[8] + (double)d.y * m[9]) + (double)d.z * m[10]));
 }
 // Ray.getPoint (math.js:297-299): origin.plus(direction.times(t))
-__device__ __forceinline__ F3 ray_point(F3 o, F3 d, double t) {
+JSRT_HD F3 ray_point(F3 o, F3 d, double t) {
     return f3(o.x + (float)((double)d.x * t), o.y + (float)((double)d.y * t), o.z + (float)((double)d.z * t));
 }
 // Vec.cartesianToSpherical (math.js:189-193)
@@ -124,7 +127,7 @@ __device__ __forceinline__ void cart_to_sph(F3 n, float &u, float &v) {
 
 // --------------------------------------------------------------------------------------------
 // geometry (geometry.js), local space
-__device__ __forceinline__ bool aabb_slab(float cx, float cy, float cz, float hx, float hy, float hz, F3 o, F3 d,
+JSRT_HD bool aabb_slab(float cx, float cy, float cz, float hx, float hy, float hz, F3 o, F3 d,
                                           double minD, double maxD, double &tmin, double &tmax) {
     // AABB.get_intersects (geometry.js:189-209)
     double t_min = -DINF, t_max = DINF;
@@ -209,11 +212,17 @@ __device__ __forceinline__ int box_enter_f32(float cx, float cy, float cz, float
     return -1;
 }
 
-__device__ __forceinline__ double plane_t(F3 o, F3 d) {  // geometry.js:246-248
+JSRT_HD double aabb_intersect(const float *c, const float *h, F3 o, F3 d, double minD, double maxD) {  // geometry.js:173-179
+    double tmin, tmax;
+    if (aabb_slab(c[0], c[1], c[2], h[0], h[1], h[2], o, d, minD, maxD, tmin, tmax)) return (tmin >= minD) ? tmin : tmax;
+    return -(double)__builtin_inf();
+}
+
+JSRT_HD double plane_t(F3 o, F3 d) {  // geometry.js:246-248
     return (d.z != 0.0f) ? -(double)o.z / (double)d.z : -DINF;
 }
 
-__device__ __forceinline__ double sphere_static(F3 o, F3 d, double minD) {  // geometry.js:429-442
+JSRT_HD double sphere_static(F3 o, F3 d, double minD) {  // geometry.js:429-442
     const double a = dot3(d, d), b = dot3(d, o), c = dot3(o, o) - 1;
     double big = b * b - a * c;
     if (big < 0 || a == 0) return -DINF;
@@ -223,7 +232,7 @@ __device__ __forceinline__ double sphere_static(F3 o, F3 d, double minD) {  // g
     return (t2 < minD) ? t1 : t2;
 }
 
-__device__ __forceinline__ double tri_intersect(const DTri &T, F3 o, F3 d) {  // geometry.js:368-375
+JSRT_HD double tri_intersect(const DTri &T, F3 o, F3 d) {  // geometry.js:368-375
     const F3 n = f3(T.n[0], T.n[1], T.n[2]);
     const double denom = dot3(n, d);
     const double distance = (denom != 0) ? (T.delta - dot3(n, o)) / denom : -DINF;
@@ -566,6 +575,8 @@ __device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
     return res;
 }
 
+#include "prim_filter.h"
+
 // --------------------------------------------------------------------------------------------
 // world intersection (world.js:7-15, 116-124; aggregates.js:14-18, 43-49, 207-225)
 struct Hit {
@@ -600,13 +611,7 @@ __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DP
         const double t = sphere_static(f3(o.x, o.y, o.z * 0.0f), f3(d.x, d.y, d.z * 0.0f), minD);
         return (fabs(oz + t * dz) <= 1) ? t : -DINF;
     }
-    case JSRT_GEOM_AABB: {  // geometry.js:173-179
-        double tmin, tmax;
-        if (aabb_slab(P.center[0], P.center[1], P.center[2], P.half[0], P.half[1], P.half[2], o, d, minD, maxD, tmin,
-                      tmax))
-            return (tmin >= minD) ? tmin : tmax;
-        return -DINF;
-    }
+    case JSRT_GEOM_AABB: return aabb_intersect(P.center, P.half, o, d, minD, maxD);
     case JSRT_GEOM_TRIANGLE:
         if (PF & PF_TRI) return tri_intersect(S.tris[P.gindex], o, d);
         return -DINF;
@@ -618,11 +623,28 @@ __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DP
 }
 
 // one row of Mat x Vec (math.js:392-397), the same operations as xf_point / xf_dir
-__device__ __forceinline__ float xf_row_point(const double *r, F3 o) {
+JSRT_HD float xf_row_point(const double *r, F3 o) {
     return (float)((((double)o.x * r[0] + (double)o.y * r[1]) + (double)o.z * r[2]) + r[3]);
 }
-__device__ __forceinline__ float xf_row_dir(const double *r, F3 d) {
+JSRT_HD float xf_row_dir(const double *r, F3 d) {
     return (float)(((double)d.x * r[0] + (double)d.y * r[1]) + (double)d.z * r[2]);
+}
+
+// SimplePlane / Square / Circle .intersect of a world ray through the primitive's inverse transform
+// `inv` (rows 0..2), for a caller that accepts minD < t < lim: a planar primitive whose plane
+// distance already fails that test may return it without transforming the x/y rows or testing its
+// bounds; the caller's decision is unchanged.
+JSRT_HD double planar_intersect(int k, const double *inv, F3 o, F3 d, double minD, double lim) {
+    // SimplePlane.intersect (geometry.js:246-248) needs only the local z row
+    const float oz = xf_row_point(inv + 8, o), dz = xf_row_dir(inv + 8, d);
+    const double t = (dz != 0.0f) ? -(double)oz / (double)dz : -(double)__builtin_inf();
+    if (k == JSRT_GEOM_PLANE || !(t > minD && t < lim)) return t;
+    const float ox = xf_row_point(inv, o), oy = xf_row_point(inv + 4, o);
+    const float dx = xf_row_dir(inv, d), dy = xf_row_dir(inv + 4, d);
+    const F3 p = ray_point(f3(ox, oy, oz), f3(dx, dy, dz), t);
+    if (k == JSRT_GEOM_SQUARE)  // geometry.js:287-291
+        return (-0.5f <= p.x && p.x <= 0.5f && -0.5f <= p.y && p.y <= 0.5f) ? t : -(double)__builtin_inf();
+    return (dot3(p, p) <= 1) ? t : -(double)__builtin_inf();  // Circle, geometry.js:310-314
 }
 
 // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast.
@@ -634,18 +656,7 @@ __device__ __forceinline__ double prim_intersect(const DScene &S, const DPrim &P
                                                  bool transp, double lim) {
     if (!transp && !P.casts_shadow) return DINF;
     const int k = P.gkind;
-    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) {
-        // SimplePlane.intersect (geometry.js:246-248) needs only the local z row
-        const float oz = xf_row_point(P.inv + 8, o), dz = xf_row_dir(P.inv + 8, d);
-        const double t = (dz != 0.0f) ? -(double)oz / (double)dz : -DINF;
-        if (k == JSRT_GEOM_PLANE || !(t > minD && t < lim)) return t;
-        const float ox = xf_row_point(P.inv, o), oy = xf_row_point(P.inv + 4, o);
-        const float dx = xf_row_dir(P.inv, d), dy = xf_row_dir(P.inv + 4, d);
-        const F3 p = ray_point(f3(ox, oy, oz), f3(dx, dy, dz), t);
-        if (k == JSRT_GEOM_SQUARE)  // geometry.js:287-291
-            return (-0.5f <= p.x && p.x <= 0.5f && -0.5f <= p.y && p.y <= 0.5f) ? t : -DINF;
-        return (dot3(p, p) <= 1) ? t : -DINF;  // Circle, geometry.js:310-314
-    }
+    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) return planar_intersect(k, P.inv, o, d, minD, lim);
     return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
 }
 
@@ -747,6 +758,23 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
     }
 }
 
+// The f32 pre-test of a top-level primitive (prim_filter.h) for the caller's (minD, lim): FLT_EXACT
+// for the kinds without one (cylinder, triangle, SDF) and for non-primitive roots.
+__device__ __forceinline__ int root_filter(const DRoot &R, F3 o, F3 d, float oabs, float dabs, const FBounds &B) {
+#ifdef JSRT_NO_PRIM_FILTER
+    return FLT_EXACT;
+#endif
+    const int k = R.p.gkind;
+    if (k != JSRT_GEOM_PLANE && k != JSRT_GEOM_SQUARE && k != JSRT_GEOM_CIRCLE && k != JSRT_GEOM_AABB &&
+        k != JSRT_GEOM_SPHERE)
+        return FLT_EXACT;
+    const FRows &F = R.fr;
+    const FRay Y = fray(F, o, d, oabs, dabs);
+    if (k == JSRT_GEOM_AABB) return aabb_filter(F, R.p.center, R.p.half, Y, B);
+    if (k == JSRT_GEOM_SPHERE) return sphere_filter(F, Y, B);
+    return planar_filter(k, F, Y, B);
+}
+
 // Conservative cull of one top-level object: false only when the object provably
 // cannot produce an accepted hit on the segment (minD, flim): the ray misses its world box inflated
 // by k|o| + e0 (flim = (float) of the far limit min(best, maxD)).
@@ -780,6 +808,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     Hit best{DINF, -1, 0};
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    const float dabs = fmaxf(fabsf(d.x), fmaxf(fabsf(d.y), fabsf(d.z)));
     const float fminD = (float)minD;
     bool live = true;
 #ifdef JSRT_DBG_COUNT
@@ -805,11 +834,23 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
 #endif
         if (!need) {  // (a divergent if, not a divergent continue: the loop itself stays uniform)
         } else if (R.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
-            if (t > minD && t < best.t && t < maxD) {
-                best = Hit{t, R.prim, 0};
-                flim = (float)best.t;
-                if (ANY) live = false;
+            // f32 pre-test first: the exact f64 test runs only for decisions too close to call
+            const double lim = fmin(maxD, best.t);
+            const int f = (!transp && !R.p.casts_shadow) ? FLT_NO : root_filter(R, o, d, oabs, dabs, fbounds(minD, maxD, lim));
+#ifdef JSRT_DBG_COUNT
+            atomicAdd(&g_dbg[100 + (ANY ? 4 : 0) + f + 1], 1ull);
+#endif
+            if (f == FLT_NO) {
+            } else if (ANY && f == FLT_YES) {  // an accepted hit; any-hit callers read only 0 < t < 1
+                best = Hit{0.5 * (minD + lim), R.prim, 0};
+                live = false;
+            } else {
+                const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, lim);
+                if (t > minD && t < best.t && t < maxD) {
+                    best = Hit{t, R.prim, 0};
+                    flim = (float)best.t;
+                    if (ANY) live = false;
+                }
             }
         } else if ((PF & PF_BVH) && R.kind == INST_BVH) {
             const double *m = R.p.inv;

@@ -341,10 +341,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
         const char *pe = getenv("JSRT_PERSIST");
         const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
-        const size_t hands = chain ? paths : level_cap;
+        // hand-off slots: one per node of a level; level 0 holds all `paths` camera rays, the
+        // deeper levels at most level_cap (k_shade poisons the batch before writing past it)
+        const size_t hands = chain ? paths : std::max(level_cap, paths);
         const size_t shadow = persist ? hands * (size_t)group : 0;
         e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
-                  : wf.reserve(pool, pool, level_cap, level_cap, true, shadow);
+                  : wf.reserve(pool, pool, hands, paths, true, shadow);
         if (e != hipSuccess) break;
         WArgs W = wf.args;
         W.ns = ns;

@@ -851,6 +851,7 @@ struct Loader {
             r.prim = in.kind == INST_PRIM ? in.prim : -1;
             if (in.kind == INST_PRIM) r.p = S.prims[in.prim];
             else memcpy(r.p.inv, &S.mats[12 * (size_t)in.matrix], sizeof r.p.inv);
+            frows_build(r.p.inv, r.fr);  // f32 view of the inverse rows for the pre-tests (prim_filter.h)
             S.rootrec.push_back(r);
         }
         for (uint32_t i = 0; i < B.n_lite; ++i) {

@@ -36,4 +36,8 @@ for name, base in (("extend", 128), ("shadow", 192)):
             tw += w
             print(f"  obj {i:2d}: lanes/ray {l / rays:.3f}  waves/wave {w / waves:.3f}  lane-util {l / (w * 64):.3f}")
     print(f"  total: object tests/ray {tl / max(rays, 1):.2f}, object passes/wave {tw / max(waves, 1):.2f}")
+for name, base in (("extend", 100), ("shadow", 104)):
+    ex, no, yes = buf[base], buf[base + 1], buf[base + 2]
+    tot = max(ex + no + yes, 1)
+    print(f"{name} f32 pre-tests: {tot} lane tests, no {no / tot:.3f} yes {yes / tot:.3f} exact {ex / tot:.4f}")
 print("stage_ms", {k: round(v, 2) for k, v in st["stage_ms"].items()})
