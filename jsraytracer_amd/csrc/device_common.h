@@ -760,14 +760,27 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
 
 // The f32 pre-test of a top-level primitive (prim_filter.h) for the caller's (minD, lim): FLT_EXACT
 // for the kinds without one (cylinder, triangle, SDF) and for non-primitive roots.
-__device__ __forceinline__ int root_filter(const DRoot &R, F3 o, F3 d, float oabs, float dabs, const FBounds &B) {
-#ifdef JSRT_NO_PRIM_FILTER
-    return FLT_EXACT;
+// Which kinds get a pre-test (bit 0 planar, 1 AABB, 2 sphere) and whether closest-hit casts use it
+// (ANY casts always do).  Off by default: A/B on MI355X (cornell) -- the top-level
+// loop is wave-uniform, so a pre-test costs every wave that needs the object its full instruction
+// count, and the exact forms (early-out after the plane distance, f64 divisions) are no dearer:
+// no pre-test 406.6 M/s, AABB 404.0, AABB + sphere 398.9, all kinds 376.8, + closest-hit 374.3.
+#ifndef JSRT_FILTER_KINDS
+#define JSRT_FILTER_KINDS 0
 #endif
+#ifndef JSRT_FILTER_CLOSEST
+#define JSRT_FILTER_CLOSEST 0
+#endif
+template <bool ANY>
+__device__ __forceinline__ bool root_filtered(int k) {
+    if (!ANY && !JSRT_FILTER_CLOSEST) return false;
+    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) return (JSRT_FILTER_KINDS & 1) != 0;
+    if (k == JSRT_GEOM_AABB) return (JSRT_FILTER_KINDS & 2) != 0;
+    if (k == JSRT_GEOM_SPHERE) return (JSRT_FILTER_KINDS & 4) != 0;
+    return false;
+}
+__device__ __forceinline__ int root_filter(const DRoot &R, F3 o, F3 d, float oabs, float dabs, const FBounds &B) {
     const int k = R.p.gkind;
-    if (k != JSRT_GEOM_PLANE && k != JSRT_GEOM_SQUARE && k != JSRT_GEOM_CIRCLE && k != JSRT_GEOM_AABB &&
-        k != JSRT_GEOM_SPHERE)
-        return FLT_EXACT;
     const FRows &F = R.fr;
     const FRay Y = fray(F, o, d, oabs, dabs);
     if (k == JSRT_GEOM_AABB) return aabb_filter(F, R.p.center, R.p.half, Y, B);
@@ -810,6 +823,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     const float dabs = fmaxf(fabsf(d.x), fmaxf(fabsf(d.y), fabsf(d.z)));
     const float fminD = (float)minD;
+    FBounds FB = fbounds(minD, maxD, maxD);  // the pre-tests' (minD, lim), lim = min(maxD, best)
     bool live = true;
 #ifdef JSRT_DBG_COUNT
     const uint64_t act0 = __ballot(1);
@@ -836,7 +850,9 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         } else if (R.kind == INST_PRIM) {
             // f32 pre-test first: the exact f64 test runs only for decisions too close to call
             const double lim = fmin(maxD, best.t);
-            const int f = (!transp && !R.p.casts_shadow) ? FLT_NO : root_filter(R, o, d, oabs, dabs, fbounds(minD, maxD, lim));
+            int f = FLT_EXACT;
+            if (!transp && !R.p.casts_shadow) f = FLT_NO;
+            else if (root_filtered<ANY>(R.p.gkind)) f = root_filter(R, o, d, oabs, dabs, FB);
 #ifdef JSRT_DBG_COUNT
             atomicAdd(&g_dbg[100 + (ANY ? 4 : 0) + f + 1], 1ull);
 #endif
@@ -849,6 +865,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
                 if (t > minD && t < best.t && t < maxD) {
                     best = Hit{t, R.prim, 0};
                     flim = (float)best.t;
+                    if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, best.t);
                     if (ANY) live = false;
                 }
             }
@@ -858,11 +875,13 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
                 flim = (float)best.t;
+                if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, best.t);
                 if (ANY) live = false;
             }
         } else if (PF & PF_AGG) {
             nested_cast<PF, ANY>(S, R.inst, o, d, minD, maxD, transp, best);
             flim = (float)(best.t < maxD ? best.t : maxD);
+            if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, fmin(maxD, best.t));
             if (ANY && best.prim >= 0) live = false;
         }
     }
