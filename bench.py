@@ -175,10 +175,12 @@ def load_pmc(config, kname):
     d = json.load(open(p)).get(config)
     if not d:
         return None, None, kname
-    hits = [k for k in d["kernels"] if k == kname or k.startswith(kname + "<")]
-    if len(hits) != 1:
+    # the stage's kernel: any template instance, or its persistent-cast form (k_extend_q: SDF scenes)
+    hits = [k for k in d["kernels"] if k.split("<")[0] in (kname, kname + "_q")]
+    if not hits:
         return None, None, kname
-    return d["kernels"][hits[0]], d.get("source"), hits[0]
+    k = max(hits, key=lambda h: d["kernels"][h].get("SQ_WAVE_CYCLES", d["kernels"][h].get("dispatches", 0)))
+    return d["kernels"][k], d.get("source"), k
 
 
 def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):

@@ -12,6 +12,8 @@
  *                          x_offset, x_delt) writing PixelBuffer RGBA8 (src/pixelbuffer.js:39-49),
  *                          progress callback({pass, completion}) (renderers.js:35,110)
  *   jsrt_render_device  <- same, device-resident outputs on a caller stream (multi-GPU tile path)
+ *   jsrt_cast           <- World.cast (src/world.js:28-30) for a batch of rays: closest-hit distance
+ *                          and the hit Primitive (known-answer tests localise parity to one cast)
  *   jsrt_scene_destroy  <- worker teardown (src/raytrace_launcher.js:106-124 terminate)
  *   jsrt_last_error     <- the reference throws strings (e.g. src/aggregates.js:39); errors here are
  *                          negative return codes + this message, never C++ exceptions.
@@ -83,6 +85,14 @@ int jsrt_render(jsrt_scene *scene, const jsrt_params *params, uint8_t *rgba8, fl
  * == x_offset) for coherent multi-GPU tiles.  Asynchronous w.r.t. the host. */
 int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
                        float *d_colors, void *hip_stream, jsrt_stats *stats);
+
+/* World.cast(ray, min_dist, max_dist, intersect_transparent) (world.js:28-30) of n rays on the scene's
+ * device: rays = n x 6 f32 host array (origin xyz with w = 1, direction xyz with w = 0, as
+ * Camera.getRayForPixel and the materials make them).  out_dist (n f64): the closest hit's distance,
+ * +Infinity for none; out_object (n i32): the hit Primitive as its OBJS index in the scene blob, -1
+ * for none.  Synchronous. */
+int jsrt_cast(jsrt_scene *scene, const float *rays, size_t n, double min_dist, double max_dist,
+              int32_t intersect_transparent, double *out_dist, int32_t *out_object);
 
 /* Number of owned columns for (W, x_offset, x_delt, col_block). */
 int32_t jsrt_owned_columns(int32_t width, int32_t x_offset, int32_t x_delt, int32_t col_block);

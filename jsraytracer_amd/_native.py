@@ -44,8 +44,8 @@ class Stats(ctypes.Structure):
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)
 
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
-EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_owned_columns",
-           "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
+EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_cast",
+           "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 # exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
@@ -93,6 +93,9 @@ def lib():
     L.jsrt_render_device.restype = ctypes.c_int
     L.jsrt_render_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
+    L.jsrt_cast.restype = ctypes.c_int
+    L.jsrt_cast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
     L.jsrt_owned_columns.restype = ctypes.c_int32
     L.jsrt_owned_columns.argtypes = [ctypes.c_int32] * 4
     L.jsrt_last_error.restype = ctypes.c_char_p

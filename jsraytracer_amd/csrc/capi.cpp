@@ -112,7 +112,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
                  o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_mcc = A.add(H.mc_const), o_lights = A.add(H.lights),
                  o_sl = A.add(H.sample_light), o_sc = A.add(H.sample_call),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
-                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg);
+                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg), o_ltris = A.add(H.ltris);
     const size_t total = A.host.size() + 256;
     HIP_TRY(hipMalloc(&sc->dmem, total));
     HIP_TRY(hipMemcpy(sc->dmem, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
@@ -145,6 +145,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.light_draws = H.light_draws;
     D.max_children = H.max_children;
     D.bvh_stack = H.bvh.empty() ? 0 : H.bvh_max_depth + 2;
+    D.ltris = (const DTri *)(b + o_ltris);
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);
@@ -336,6 +337,38 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
 }  // namespace
 
 extern "C" {
+
+int jsrt_cast(jsrt_scene *s, const float *rays, size_t n, double min_dist, double max_dist, int32_t intersect_transparent,
+              double *out_dist, int32_t *out_object) {
+    if (!s) return set_error(-1, "scene is NULL");
+    if (n == 0) return 0;
+    if (!rays || !out_dist || !out_object) return set_error(-1, "NULL buffer");
+    if (n > (size_t)UINT32_MAX / 8) return set_error(-1, "too many rays");
+    HIP_TRY(hipSetDevice(s->device));
+    float *d_rays = nullptr;
+    double *d_t = nullptr;
+    int32_t *d_prim = nullptr;
+    auto cleanup = [&] {
+        if (d_rays) (void)hipFree(d_rays);
+        if (d_t) (void)hipFree(d_t);
+        if (d_prim) (void)hipFree(d_prim);
+    };
+    hipError_t e = hipMalloc(&d_rays, n * 6 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_t, n * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&d_prim, n * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = cast_rays(s->ds, d_rays, (uint32_t)n, min_dist, max_dist, intersect_transparent != 0, d_t, d_prim, 0);
+    if (e == hipSuccess) e = hipMemcpy(out_dist, d_t, n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_object, d_prim, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) return set_error(-3, std::string("jsrt_cast: ") + hipGetErrorString(e));
+    const std::vector<int32_t> &po = s->hs.prim_obj;
+    for (size_t i = 0; i < n; ++i) {
+        const int32_t p = out_object[i];
+        out_object[i] = (p >= 0 && (size_t)p < po.size()) ? po[p] : -1;
+    }
+    return 0;
+}
 
 int jsrt_render(jsrt_scene *s, const jsrt_params *p, uint8_t *rgba8, float *colors_f32, jsrt_progress_fn progress,
                 void *user, jsrt_stats *stats) {

@@ -696,7 +696,7 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                 const int cnt = ~N.b;
                 for (int k = 0; k < cnt; ++k) {
                     double t;
-                    if (fast) t = tri_intersect(S.tris[S.leaf_tris[N.a + k]], o, d);
+                    if (fast) t = tri_intersect(S.ltris[N.a + k], o, d);  // leaf-ordered copy: no index load
                     else t = prim_intersect<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp, fmin(maxD, best.t));
                     if (t > minD && t < maxD && t < best.t) {
                         best.t = t;

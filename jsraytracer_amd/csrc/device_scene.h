@@ -197,7 +197,11 @@ struct DScene {
     int32_t light_draws;     // RNG draws of all light samples of a node (scatter draws follow)
     int32_t max_children;    // most children one ray-tree node can spawn (0..2)
     int32_t bvh_stack;       // LDS traversal-stack entries per lane (deepest BVH node + 2; 0: no BVH)
-    int32_t pad;
+    const DTri *ltris;       // parallel to leaf_prims: the triangle of a fast leaf entry (leaf order)
 };
+
+// Dynamic LDS of a casting kernel over a scene with BVHs: per lane a traversal stack of bvh_stack
+// 4-byte entries (device_common.h bvh_cast).
+inline size_t bvh_lds_bytes(const DScene &S, int block) { return (size_t)S.bvh_stack * block * 4; }
 
 }  // namespace jsrt

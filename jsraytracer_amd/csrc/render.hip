@@ -286,6 +286,28 @@ extern template void run_batch<PF_ALL, true>(const DScene &, const RenderArgs &,
 extern template void run_batch<PF_ALL, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
                                          KernelTimes *, const std::vector<size_t> &);
 
+#define JSRT_CAST_EXTERN(PFV) \
+    extern template void cast_rays_pf<PFV>(const DScene &, const float *, uint32_t, double, double, int, double *, \
+                                           int32_t *, hipStream_t);
+JSRT_CAST_EXTERN(PF_ANALYTIC)
+JSRT_CAST_EXTERN(PF_MESH)
+JSRT_CAST_EXTERN(PF_SDF)
+JSRT_CAST_EXTERN(PF_ALL)
+#undef JSRT_CAST_EXTERN
+
+hipError_t cast_rays(const DScene &S, const float *d_rays, uint32_t n, double min_dist, double max_dist, bool transparent,
+                     double *d_t, int32_t *d_prim, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const int tr = transparent ? 1 : 0;
+    switch (S.profile) {
+    case PF_ANALYTIC: cast_rays_pf<PF_ANALYTIC>(S, d_rays, n, min_dist, max_dist, tr, d_t, d_prim, st); break;
+    case PF_MESH: cast_rays_pf<PF_MESH>(S, d_rays, n, min_dist, max_dist, tr, d_t, d_prim, st); break;
+    case PF_SDF: cast_rays_pf<PF_SDF>(S, d_rays, n, min_dist, max_dist, tr, d_t, d_prim, st); break;
+    default: cast_rays_pf<PF_ALL>(S, d_rays, n, min_dist, max_dist, tr, d_t, d_prim, st); break;
+    }
+    return hipGetLastError();
+}
+
 namespace {
 template <bool CHAIN>
 void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,

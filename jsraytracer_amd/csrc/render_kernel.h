@@ -124,6 +124,11 @@ size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth);
 // renderers.js:93-98): the image IncrementalMultisamplingRenderer holds after pass passes-1.
 hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st);
 
+// World.cast (world.js:28-30) of n rays (device buffers: n x 6 f32 rays, origin w = 1, direction
+// w = 0): closest-hit distance and DPrim index (-1: none).  The jsrt_cast entry (known-answer tests).
+hipError_t cast_rays(const DScene &S, const float *d_rays, uint32_t n, double min_dist, double max_dist, bool transparent,
+                     double *d_t, int32_t *d_prim, hipStream_t st);
+
 // Owned column c -> image column px (see jsrt.h jsrt_render_device).
 __host__ __device__ inline int32_t owned_to_px(int32_t c, int32_t x_offset, int32_t x_delt, int32_t col_block) {
     if (col_block <= 1) return x_offset + c * x_delt;

@@ -731,6 +731,26 @@ __global__ __launch_bounds__(256) void k_shadow_sum(DScene S, WArgs W, int L) {
     if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
 
+// World.cast of a batch of independent rays (jsrt_cast): the closest-hit cast k_extend runs,
+// with the caller's (minD, maxD, intersectTransparent).
+template <int PF>
+__global__ __launch_bounds__(256) void k_cast_rays(DScene S, const float *rays, uint32_t n, double minD, double maxD,
+                                                   int transp, double *out_t, int32_t *out_prim) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + 6 * (size_t)i;
+    const F3 o = f3(r[0], r[1], r[2]), d = f3(r[3], r[4], r[5]);
+    const Hit h = world_cast<PF, false>(S, o, d, minD, maxD, transp != 0);
+    out_t[i] = h.t;
+    out_prim[i] = h.prim;
+}
+template <int PF>
+void cast_rays_pf(const DScene &S, const float *rays, uint32_t n, double minD, double maxD, int transp, double *t,
+                  int32_t *prim, hipStream_t st) {
+    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? bvh_lds_bytes(S, 256) : 0;
+    hipLaunchKernelGGL((k_cast_rays<PF>), dim3(grid_ub(n)), dim3(256), lds, st, S, rays, n, minD, maxD, transp, t, prim);
+}
+
 // Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.
 // Tree: level L's launches cover bound[L] rays (the real count is on the device and surplus
 // blocks exit at once; a count above the bound sets LVL_UNDER and the frame is redone);
@@ -745,7 +765,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         if (ev) kt->ev[which].end(st);
     };
     // dynamic LDS of the casting kernels: the BVH traversal stack (bvh_cast), 256 lanes x entries
-    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? (size_t)S.bvh_stack * 256 * sizeof(int) : 0;
+    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? bvh_lds_bytes(S, 256) : 0;
     // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
     const bool Q = (PF & PF_SDF) && W.sstride != 0;
     if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);

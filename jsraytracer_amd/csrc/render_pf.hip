@@ -11,6 +11,8 @@ template void run_batch<JSRT_PF, true>(const DScene &, const RenderArgs &, const
                                        const std::vector<size_t> &);
 template void run_batch<JSRT_PF, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t, KernelTimes *,
                                         const std::vector<size_t> &);
+template void cast_rays_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double, double, int, double *, int32_t *,
+                                   hipStream_t);
 
 // A/B instrumentation (variant builds with -DJSRT_DBG_COUNT for one profile): the counters live in
 // this profile's code object, so they are read back from here (tools/dbg_counts.py)

@@ -318,6 +318,7 @@ struct Loader {
         }
         int32_t idx = (int32_t)S.prims.size();
         S.prims.push_back(p);
+        S.prim_obj.push_back(o);
         prim_of_obj[o] = idx;
         LBox lb;
         lb.bounded = true;
@@ -394,6 +395,16 @@ struct Loader {
         }
         S.bvh[idx] = d;
         return idx;
+    }
+
+    // ---- leaf-ordered triangles ----
+    // Copies each fast leaf's triangle into leaf order (ltris, parallel to leaf_prims), so a leaf test
+    // loads its record without first loading its index (one dependent load less per leaf visit).
+    // (Renumbering the nodes greater-first for locality was measured too: no effect, r02_s6.)
+    void leaf_triangles() {
+        S.ltris.assign(S.leaf_tris.size(), DTri{});
+        for (size_t i = 0; i < S.leaf_tris.size(); ++i)
+            if (S.leaf_tris[i] >= 0) S.ltris[i] = S.tris[S.leaf_tris[i]];
     }
 
     // ---- SDF (sdf.js) -> program (sdf_program.h) ----
@@ -930,6 +941,7 @@ struct Loader {
             S.max_children = std::max(S.max_children, n);
         }
         shading_matrices();
+        leaf_triangles();
         S.profile = f == 0 ? PF_ANALYTIC : (f & ~PF_MESH) == 0 ? PF_MESH : (f & ~PF_SDF) == 0 ? PF_SDF : PF_ALL;
         for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);
         if (B.n_sdf) S.sdf_child.assign(B.chld, B.chld + B.n_chld);

@@ -11,6 +11,7 @@ namespace jsrt {
 
 struct HostScene {
     std::vector<DPrim> prims;
+    std::vector<int32_t> prim_obj;     // per DPrim: its OBJS index in the blob (jsrt_cast)
     std::vector<DInst> insts;
     std::vector<int32_t> inst_child, roots;
     std::vector<RootBound> rbounds;
@@ -19,6 +20,7 @@ struct HostScene {
     std::vector<DBvhNode> bvh;
     std::vector<int32_t> leaf_prims, leaf_tris;
     std::vector<DTri> tris;
+    std::vector<DTri> ltris;       // parallel to leaf_prims: tris[leaf_tris[i]] (zero record if none)
     std::vector<DTriShade> trish;
     std::vector<jsrt_rec_material> mat;
     std::vector<int32_t> mat_flags;    // MATF_* per material

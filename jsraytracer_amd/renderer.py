@@ -52,6 +52,18 @@ class Scene:
         self._h = h
         self.device = device
 
+    def cast(self, rays, min_dist=0.0, max_dist=float("inf"), intersect_transparent=True):
+        """World.cast (world.js:28-30) of rays (n x 6 f32: origin xyz w=1, direction xyz w=0) on the
+        device: (distance f64, hit Primitive's OBJS index i32, -1 none) per ray."""
+        import numpy as np
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        n = len(rays)
+        t = np.empty(n, np.float64)
+        obj = np.empty(n, np.int32)
+        check(_native.lib().jsrt_cast(self._h, rays.ctypes.data, n, min_dist, max_dist, int(bool(intersect_transparent)),
+                                      t.ctypes.data, obj.ctypes.data), "jsrt_cast")
+        return t, obj
+
     def close(self):
         if getattr(self, "_h", None):
             _native.lib().jsrt_scene_destroy(self._h)

@@ -1326,3 +1326,29 @@ int jsrt_oracle_render(const void *blob, size_t blob_bytes, const jsrt_oracle_pa
     free(th);
     return rc;
 }
+
+/* World.cast (world.js:28-30) of a batch of rays: rays n x (origin xyz, direction xyz) f32 with
+ * origin w = 1 and direction w = 0 (as Camera.getRayForPixel and the materials make them).  Writes the
+ * closest hit's distance (+Infinity: none) and its Primitive's OBJS index (-1: none). */
+int jsrt_oracle_cast(const void *blob, size_t blob_bytes, const float *rays, size_t n, double min_dist,
+                     double max_dist, int32_t transparent, double *out_t, int32_t *out_obj) {
+    Scene S;
+    if (parse_scene(blob, blob_bytes, &S)) return -1;
+    Ctx *C = (Ctx *)calloc(1, sizeof(Ctx));
+    if (!C) return -2;
+    C->S = &S;
+    for (size_t i = 0; i < n; ++i) {
+        const float *r = rays + 6 * i;
+        Ray ray = {vof4(r[0], r[1], r[2], 1), vof4(r[3], r[4], r[5], 0)};
+        const Hit h = world_cast(C, ray, min_dist, max_dist, transparent != 0);
+        out_t[i] = h.distance;
+        out_obj[i] = h.object;
+    }
+    const int err = C->err;
+    free(C);
+    if (err) {
+        set_err("cast failed");
+        return -3;
+    }
+    return 0;
+}

@@ -59,6 +59,10 @@ def lib():
         L.jsrt_oracle_rng.argtypes = [ctypes.c_uint32] * 5
         L.jsrt_oracle_mix.restype = ctypes.c_uint32
         L.jsrt_oracle_mix.argtypes = [ctypes.c_uint32] * 2
+        L.jsrt_oracle_cast.restype = ctypes.c_int
+        L.jsrt_oracle_cast.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -115,6 +119,38 @@ def golden_image(tag, width, height):
 def golden_kats():
     with open(os.path.join(GOLDEN, "kats.json")) as f:
         return json.load(f)
+
+
+def cast(blob, rays, min_dist=0.0, max_dist=float("inf"), transparent=True):
+    """World.cast (world.js:28-30) of rays (n x 6 f32: origin xyz w=1, direction xyz w=0):
+    (distance f64, hit Primitive's OBJS index i32, -1 none)."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    n = len(rays)
+    t = np.empty(n, np.float64)
+    obj = np.empty(n, np.int32)
+    L = lib()
+    if L.jsrt_oracle_cast(bytes(blob), len(blob), rays.ctypes.data, n, min_dist, max_dist, int(bool(transparent)),
+                          t.ctypes.data, obj.ctypes.data):
+        raise RuntimeError(L.jsrt_oracle_last_error().decode())
+    return t, obj
+
+
+def golden_casts(name):
+    """World.cast known answers computed by the reference (oracle/refharness/make_cast_kats.js):
+    {"blob_sha256", "sets": [{name, minD, maxD, transp, rays (n x 6 f32), t (f64), obj (i32)}]}."""
+    import base64
+    with gzip.open(os.path.join(GOLDEN, "casts", name + ".json.gz"), "rt") as f:
+        d = json.load(f)
+    for s in d["sets"]:
+        s["maxD"] = float(s["maxD"])
+        s["rays"] = np.frombuffer(base64.b64decode(s["rays"]), np.float32).reshape(-1, 6)
+        s["t"] = np.frombuffer(base64.b64decode(s["t"]), np.float64)
+        s["obj"] = np.frombuffer(base64.b64decode(s["obj"]), np.int32)
+    return d
+
+
+def golden_cast_scenes():
+    return sorted(f[:-len(".json.gz")] for f in os.listdir(os.path.join(GOLDEN, "casts")) if f.endswith(".json.gz"))
 
 
 # ---- mesh fixtures (oracle/refharness/regen_mesh_fixtures.sh): skeleton + OBJ + MTL per scene ----
