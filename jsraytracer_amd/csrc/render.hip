@@ -193,6 +193,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
     bytes += need(7 * hands, 16) + need(64, 4);                      // hand-off + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
+    if (tree) bytes += need(MAX_TREE_DEPTH * 2 * BKT_N, 4);          // hit-primitive buckets
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
     } else {
         if (mem) (void)hipFree(mem);
@@ -217,6 +218,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
+    if (tree) w.bkt = carve<uint32_t>(p, MAX_TREE_DEPTH * 2 * BKT_N);
     w.nstride = nodes;
     w.hstride = hands;
     w.sstride = shadow;
@@ -374,6 +376,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         W.ns = ns;
         W.group = group;
         W.chain = chain ? 1 : 0;
+        // shadow hand-off bucketed by hit primitive: flat scenes of few primitives, one lane per sample
+        const char *be = getenv("JSRT_BUCKET");
+        W.bucket = (!chain && !persist && S.all_roots_prims && S.n_prims <= BKT_N && ns > 0 && ns <= 64 &&
+                    !(be && be[0] == '0')) ? 1 : 0;
         W.pool = pool;
         W.level_cap = level_cap;
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;

@@ -70,6 +70,25 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
+// Block-aggregated atomicAdd(&ctr[key], 1) for the threads with want (key < BKT_N): an LDS
+// histogram, then one global atomic per key present in the block (same-address global atomics
+// serialise device-wide, so one per thread or per wave is far too many).  Returns the thread's old
+// value (its slot).  Every thread of the block must call it.
+template <int NT>
+__device__ __forceinline__ uint32_t block_claim(uint32_t *ctr, int key, bool want) {
+    __shared__ uint32_t hist[BKT_N], hbase[BKT_N];
+    if (threadIdx.x < BKT_N) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t rank = want ? atomicAdd(&hist[key], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < BKT_N) {
+        const uint32_t c = hist[threadIdx.x];
+        hbase[threadIdx.x] = c ? atomicAdd(ctr + threadIdx.x, c) : 0u;
+    }
+    __syncthreads();
+    return want ? hbase[key] + rank : 0u;
+}
+
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
     if (p == DEAD_RAY) return;
@@ -118,6 +137,7 @@ struct Handoff {
     double kr, smoothness;
     int32_t mkind;
     uint32_t addr, key;
+    uint32_t node;  // the node's level index (bucketed hand-off: where k_shadow writes its colour)
 };
 struct NodeOut {
     F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
@@ -391,7 +411,7 @@ __device__ __forceinline__ void store_hand(const WArgs &W, uint32_t h, const Han
     p[3 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f(o.addr));
     p[4 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(o.key));
     p[5 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2loint(o.smoothness)));
-    p[6 * hs] = make_float4(u2f((uint32_t)__double2hiint(o.smoothness)), 0.0f, 0.0f, 0.0f);
+    p[6 * hs] = make_float4(u2f((uint32_t)__double2hiint(o.smoothness)), u2f(o.node), 0.0f, 0.0f);
 }
 
 // per pixel, the renderer's f32 accumulation of one sample (renderers.js:93-97, 52-61)
@@ -419,20 +439,42 @@ template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L, double minD) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     uint32_t i = t;
+    bool live = true;
     if (CHAIN) {
         if (t >= W.npaths) return;
     } else {
         const LevelRange R = level_range(W, L);
         if (t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // the launch bound was too small
-        if (t >= R.count) return;
-        i = R.base + t;
+        if (W.bucket) {  // every thread reaches block_claim below
+            if (blockIdx.x * 256u >= R.count) return;  // block-uniform
+            live = t < R.count;
+        } else if (t >= R.count) {
+            return;
+        }
+        i = R.base + (live ? t : 0u);
     }
-    if (W.prim[i] == NO_RAY) return;
-    const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
-    const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
-    W.t[i] = h.t;
-    W.prim[i] = h.prim;
-    W.ctx[i] = h.ctx;
+    live = live && W.prim[i] != NO_RAY;
+    int hp = -1;
+    if (live) {
+        const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
+        const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
+        W.t[i] = h.t;
+        W.prim[i] = h.prim;
+        W.ctx[i] = h.ctx;
+        hp = h.prim;
+    }
+    if (!CHAIN && W.bucket) (void)block_claim<256>(W.bkt + (size_t)(2 * L) * BKT_N, hp, hp >= 0);  // bucket sizes
+}
+
+// Bucketed shadow hand-off (WArgs::bucket): the lit nodes of level L are written grouped by hit
+// primitive -- bucket p starts after the hits of primitives 0..p-1 (counted by k_extend) -- so the
+// 64 lanes of a k_shadow wave serve nodes on one surface: their shadow rays cull the same objects
+// and their materials take the same branches.  Only the order k_shadow visits nodes in changes.
+__device__ __forceinline__ uint32_t bucket_start(const DScene &S, const WArgs &W, int L, int p) {
+    const CONST_AS uint32_t *cnt = as_const(W.bkt + (size_t)(2 * L) * BKT_N);
+    uint32_t off = 0;
+    for (int j = 0; j < S.n_prims; ++j) off += j < p ? cnt[j] : 0u;
+    return off;
 }
 
 // World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
@@ -477,7 +519,8 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         const Hit h{W.t[r], prim, W.ctx[r]};
         nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
         store_node(W, i, out.surf, out.info);
-        if (out.info & INFO_LIT) store_hand(W, q, out.h);
+        out.h.node = q;
+        if ((out.info & INFO_LIT) && (CHAIN || !W.bucket)) store_hand(W, q, out.h);
         if (nchild > 0) store_child(W, i, 0, ch0);
         if (nchild > 1) store_child(W, i, 1, ch1);
     }
@@ -491,6 +534,11 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
             W.prim[r] = NO_RAY;  // no child, or children black without a cast (depth 0)
         }
         return;
+    }
+    if (W.bucket) {  // the lit node's hand-off into its primitive's bucket (see bucket_start)
+        const bool lit = hit && (out.info & INFO_LIT);
+        const uint32_t k = block_claim<256>(W.bkt + (size_t)(2 * L + 1) * BKT_N, prim, lit);
+        if (lit) store_hand(W, bucket_start(S, W, L, prim) + k, out.h);
     }
     // tree: children append to level L + 1; at depth 0 they are black without a cast
     const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
@@ -598,12 +646,26 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     }
     const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t q = e / G, s = e % G;  // G is a power of two
-    const bool in = q < count;
+    uint32_t q = e / G;  // G is a power of two
+    const uint32_t s = e % G;
+    bool in = q < count;
+    const float4 *hp = W.hand + (in ? q : 0u);
+    if (!CHAIN && !SERIAL && W.bucket) {  // hand-off slot q: a lit node if its bucket has filled it
+        const CONST_AS uint32_t *cnt = as_const(W.bkt + (size_t)(2 * L) * BKT_N);
+        const CONST_AS uint32_t *fill = as_const(W.bkt + (size_t)(2 * L + 1) * BKT_N);
+        uint32_t off = 0;
+        bool filled = false;
+        for (int j = 0; j < S.n_prims; ++j) {
+            const uint32_t c = cnt[j];
+            filled = filled || (q >= off && q < off + fill[j]);
+            off += c;
+        }
+        in = in && filled;
+        q = in ? f2u(hp[6 * W.hstride].y) : 0u;
+    }
     const uint32_t i = base + (in ? q : 0u);
     const float4 nd = W.node[i];
     const bool lit = in && (f2u(nd.w) & INFO_LIT);
-    const float4 *hp = W.hand + (in ? q : 0u);
     F3 ret = f3(nd.x, nd.y, nd.z);  // ambient
     if (SERIAL) {  // one lane per node: every sample in order
         if (!lit) return;
@@ -769,6 +831,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
     // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
     const bool Q = (PF & PF_SDF) && W.sstride != 0;
     if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
+    if (!CHAIN && W.bucket) (void)hipMemsetAsync(W.bkt, 0, (size_t)MAX_TREE_DEPTH * 2 * BKT_N * sizeof(uint32_t), st);
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
     std::vector<size_t> ubs;  // launch bound of each level's ray count
     for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
