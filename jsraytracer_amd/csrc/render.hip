@@ -376,10 +376,11 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         W.ns = ns;
         W.group = group;
         W.chain = chain ? 1 : 0;
-        // shadow hand-off bucketed by hit primitive: flat scenes of few primitives, one lane per sample
+        // shadow hand-off bucketed by hit primitive (<= BKT_N buckets of consecutive primitives)
         const char *be = getenv("JSRT_BUCKET");
-        W.bucket = (!chain && !persist && S.all_roots_prims && S.n_prims <= BKT_N && ns > 0 && ns <= 64 &&
-                    !(be && be[0] == '0')) ? 1 : 0;
+        int shift = 0;
+        while (S.n_prims > 0 && ((S.n_prims - 1) >> shift) >= BKT_N) ++shift;
+        W.bucket = (!chain && !persist && S.n_prims > 0 && ns > 0 && ns <= 64 && !(be && be[0] == '0')) ? shift + 1 : 0;
         W.pool = pool;
         W.level_cap = level_cap;
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;

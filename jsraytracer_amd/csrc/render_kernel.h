@@ -13,7 +13,7 @@ namespace jsrt {
 constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of the breadth-first schedule)
 constexpr int LVL_FLAG = 63;        // WArgs::lvl word set when a batch outgrew its pool (frame redone)
 constexpr int LVL_UNDER = 62;       // WArgs::lvl word set when a level outgrew its launch bound
-constexpr int BKT_N = 64;           // most primitives of a scene whose shadow hand-off is bucketed
+constexpr int BKT_N = 64;           // buckets of the shadow hand-off (hit primitive >> shift)
 
 struct RenderArgs {
     int32_t W, H, kind, max_depth;
@@ -60,15 +60,15 @@ struct WArgs {
     uint32_t *qctr;
     float4 *sray;      // [e] {P.xyz, -}, [sstride + e] {delta.xyz, -}
     float4 *scol;      // [e] {unshadowed colour.xyz, state: 0 no cast / lit, 1 cast pending, 2 shadowed}
-    // hit-primitive buckets of the lit nodes per level (W.bucket): [(L * 2 + 0) * BKT_N + p] hits on
-    // primitive p (k_extend), [(L * 2 + 1) * BKT_N + p] hand-offs written so far in its bucket (k_shade)
+    // hit-primitive buckets of the lit nodes per level (W.bucket): [(L * 2 + 0) * BKT_N + b] hits in
+    // bucket b (k_extend), [(L * 2 + 1) * BKT_N + b] hand-offs written so far in it (k_shade)
     uint32_t *bkt;
     // batch
     uint32_t p0, npix, s0, npaths;
     int32_t ns;        // light samples per lit node
     int32_t group;     // lanes per node in k_shadow: a power of two >= ns (<= 64), or 1 (serial)
     int32_t chain;     // schedule
-    int32_t bucket;    // tree schedule, flat scene: k_shadow reads lit nodes bucketed by hit primitive (bkt)
+    int32_t bucket;    // tree schedule: 0, or 1 + shift: k_shadow reads lit nodes bucketed by hit primitive >> shift (bkt)
     size_t pool, level_cap;
     size_t nstride, hstride;  // plane strides of child / slot and of hand
     size_t sstride;           // entries of sray / scol (0: persistent casts not used)

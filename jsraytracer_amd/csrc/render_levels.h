@@ -463,17 +463,21 @@ __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs
         W.ctx[i] = h.ctx;
         hp = h.prim;
     }
-    if (!CHAIN && W.bucket) (void)block_claim<256>(W.bkt + (size_t)(2 * L) * BKT_N, hp, hp >= 0);  // bucket sizes
+    if (!CHAIN && W.bucket) (void)block_claim<256>(W.bkt + (size_t)(2 * L) * BKT_N, hp >> (W.bucket - 1), hp >= 0);
 }
 
-// Bucketed shadow hand-off (WArgs::bucket): the lit nodes of level L are written grouped by hit
-// primitive -- bucket p starts after the hits of primitives 0..p-1 (counted by k_extend) -- so the
-// 64 lanes of a k_shadow wave serve nodes on one surface: their shadow rays cull the same objects
-// and their materials take the same branches.  Only the order k_shadow visits nodes in changes.
-__device__ __forceinline__ uint32_t bucket_start(const DScene &S, const WArgs &W, int L, int p) {
+// Bucketed shadow hand-off (WArgs::bucket = shift + 1): the lit nodes of level L are written grouped
+// by hit primitive (bucket prim >> shift: one primitive each in a flat scene, runs of consecutive
+// triangles in a mesh) -- bucket b starts after the hits of buckets 0..b-1 (counted by k_extend) --
+// so the 64 lanes of a k_shadow wave serve nodes on one surface: their shadow rays cull the same
+// objects and walk the same BVH nodes, and their materials take the same branches.  Only the order
+// k_shadow visits nodes in changes.
+__device__ __forceinline__ int bucket_count(const DScene &S, const WArgs &W) { return ((S.n_prims - 1) >> (W.bucket - 1)) + 1; }
+__device__ __forceinline__ uint32_t bucket_start(const DScene &S, const WArgs &W, int L, int b) {
     const CONST_AS uint32_t *cnt = as_const(W.bkt + (size_t)(2 * L) * BKT_N);
     uint32_t off = 0;
-    for (int j = 0; j < S.n_prims; ++j) off += j < p ? cnt[j] : 0u;
+    const int nb = bucket_count(S, W);
+    for (int j = 0; j < nb; ++j) off += j < b ? cnt[j] : 0u;
     return off;
 }
 
@@ -537,8 +541,9 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
     }
     if (W.bucket) {  // the lit node's hand-off into its primitive's bucket (see bucket_start)
         const bool lit = hit && (out.info & INFO_LIT);
-        const uint32_t k = block_claim<256>(W.bkt + (size_t)(2 * L + 1) * BKT_N, prim, lit);
-        if (lit) store_hand(W, bucket_start(S, W, L, prim) + k, out.h);
+        const int b = lit ? prim >> (W.bucket - 1) : 0;
+        const uint32_t k = block_claim<256>(W.bkt + (size_t)(2 * L + 1) * BKT_N, b, lit);
+        if (lit) store_hand(W, bucket_start(S, W, L, b) + k, out.h);
     }
     // tree: children append to level L + 1; at depth 0 they are black without a cast
     const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
@@ -655,7 +660,8 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
         const CONST_AS uint32_t *fill = as_const(W.bkt + (size_t)(2 * L + 1) * BKT_N);
         uint32_t off = 0;
         bool filled = false;
-        for (int j = 0; j < S.n_prims; ++j) {
+        const int nb = bucket_count(S, W);
+        for (int j = 0; j < nb; ++j) {
             const uint32_t c = cnt[j];
             filled = filled || (q >= off && q < off + fill[j]);
             off += c;
