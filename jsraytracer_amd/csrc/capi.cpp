@@ -112,7 +112,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
                  o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_mcc = A.add(H.mc_const), o_lights = A.add(H.lights),
                  o_sl = A.add(H.sample_light), o_sc = A.add(H.sample_call),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
-                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg), o_ltris = A.add(H.ltris);
+                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg), o_ltris = A.add(H.ltris), o_plit = A.add(H.prim_lit);
     const size_t total = A.host.size() + 256;
     HIP_TRY(hipMalloc(&sc->dmem, total));
     HIP_TRY(hipMemcpy(sc->dmem, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
@@ -146,6 +146,7 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.max_children = H.max_children;
     D.bvh_stack = H.bvh.empty() ? 0 : H.bvh_max_depth + 2;
     D.ltris = (const DTri *)(b + o_ltris);
+    D.prim_lit = (const int32_t *)(b + o_plit);
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);

@@ -198,6 +198,7 @@ struct DScene {
     int32_t max_children;    // most children one ray-tree node can spawn (0..2)
     int32_t bvh_stack;       // LDS traversal-stack entries per lane (deepest BVH node + 2; 0: no BVH)
     const DTri *ltris;       // parallel to leaf_prims: the triangle of a fast leaf entry (leaf order)
+    const int32_t *prim_lit; // per prim: 1 if its material takes light samples (not Solid / Transparent)
 };
 
 // Dynamic LDS of a casting kernel over a scene with BVHs: per lane a traversal stack of bvh_stack

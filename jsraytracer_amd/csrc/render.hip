@@ -84,6 +84,28 @@ __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
     write_result(W, i, c);
 }
 
+__global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L) {
+    __shared__ uint32_t part[256];
+    uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
+    constexpr int PER = BKT_K / 256;
+    const int t = (int)threadIdx.x;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { c[j] = B[t * PER + j]; sum += c[j]; }
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {  // inclusive scan of the per-thread sums
+        const uint32_t v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t off = part[t] - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { B[2 * BKT_K + t * PER + j] = off; off += c[j]; }
+    if (t == 255) B[3 * BKT_K] = part[255];
+}
+
 // tree schedule: per pixel, the batch's samples in order
 __global__ __launch_bounds__(256) void k_accum(RenderArgs A, WArgs W) {
     const uint32_t pl = blockIdx.x * 256 + threadIdx.x;
@@ -193,7 +215,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
     bytes += need(7 * hands, 16) + need(64, 4);                      // hand-off + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
-    if (tree) bytes += need(MAX_TREE_DEPTH * 2 * BKT_N, 4);          // hit-primitive buckets
+    if (tree) bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);  // buckets
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
     } else {
         if (mem) (void)hipFree(mem);
@@ -218,7 +240,11 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
-    if (tree) w.bkt = carve<uint32_t>(p, MAX_TREE_DEPTH * 2 * BKT_N);
+    if (tree) {
+        w.bkt = carve<uint32_t>(p, MAX_TREE_DEPTH * BKT_LEVEL);
+        w.bbase = carve<uint32_t>(p, (hands / 256 + 1) * BKT_N);
+        w.brank = carve<uint32_t>(p, rays);
+    }
     w.nstride = nodes;
     w.hstride = hands;
     w.sstride = shadow;

@@ -14,6 +14,9 @@ constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of th
 constexpr int LVL_FLAG = 63;        // WArgs::lvl word set when a batch outgrew its pool (frame redone)
 constexpr int LVL_UNDER = 62;       // WArgs::lvl word set when a level outgrew its launch bound
 constexpr int BKT_N = 64;           // buckets of the shadow hand-off (hit primitive >> shift)
+constexpr int BKT_S = 16;           // slices per bucket (block index % BKT_S): spreads the counters' atomics
+constexpr int BKT_K = BKT_N * BKT_S;  // counters per level, key = bucket * BKT_S + slice
+constexpr int BKT_LEVEL = 3 * BKT_K + 64;  // words per level: counts, (spare), offsets (+ total)
 
 struct RenderArgs {
     int32_t W, H, kind, max_depth;
@@ -60,9 +63,12 @@ struct WArgs {
     uint32_t *qctr;
     float4 *sray;      // [e] {P.xyz, -}, [sstride + e] {delta.xyz, -}
     float4 *scol;      // [e] {unshadowed colour.xyz, state: 0 no cast / lit, 1 cast pending, 2 shadowed}
-    // hit-primitive buckets of the lit nodes per level (W.bucket): [(L * 2 + 0) * BKT_N + b] hits in
-    // bucket b (k_extend), [(L * 2 + 1) * BKT_N + b] hand-offs written so far in it (k_shade)
+    // hit-primitive buckets of the lit nodes per level (W.bucket), BKT_LEVEL words from L * BKT_LEVEL:
+    // [k] lit nodes of key k (k_extend), [2 BKT_K + k] its first hand-off slot (k_bucket_offsets),
+    // [3 BKT_K] the level's lit nodes
     uint32_t *bkt;
+    uint32_t *bbase;   // [block * BKT_N + bucket]: the block's first slot in its key's range (k_extend)
+    uint32_t *brank;   // [ray]: a lit hit's rank among its block's hits in its bucket (k_extend)
     // batch
     uint32_t p0, npix, s0, npaths;
     int32_t ns;        // light samples per lit node

@@ -70,25 +70,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
-// Block-aggregated atomicAdd(&ctr[key], 1) for the threads with want (key < BKT_N): an LDS
-// histogram, then one global atomic per key present in the block (same-address global atomics
-// serialise device-wide, so one per thread or per wave is far too many).  Returns the thread's old
-// value (its slot).  Every thread of the block must call it.
-template <int NT>
-__device__ __forceinline__ uint32_t block_claim(uint32_t *ctr, int key, bool want) {
-    __shared__ uint32_t hist[BKT_N], hbase[BKT_N];
-    if (threadIdx.x < BKT_N) hist[threadIdx.x] = 0u;
-    __syncthreads();
-    const uint32_t rank = want ? atomicAdd(&hist[key], 1u) : 0u;
-    __syncthreads();
-    if (threadIdx.x < BKT_N) {
-        const uint32_t c = hist[threadIdx.x];
-        hbase[threadIdx.x] = c ? atomicAdd(ctr + threadIdx.x, c) : 0u;
-    }
-    __syncthreads();
-    return want ? hbase[key] + rank : 0u;
-}
-
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
     if (p == DEAD_RAY) return;
@@ -434,9 +415,20 @@ unsigned persistent_grid(const void *kernel, size_t work);
 inline unsigned grid(size_t n) { return (unsigned)((n + 255) / 256); }
 inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 255) / 256); }
 
+// Bucketed shadow hand-off (WArgs::bucket = shift + 1): the lit nodes of level L are written grouped
+// by hit primitive (bucket prim >> shift: one primitive each in a flat scene, runs of consecutive
+// triangles in a mesh; within a bucket by slice), so the 64 lanes of a k_shadow wave serve nodes on
+// one surface: their shadow rays cull the same objects and walk the same BVH nodes, and their
+// materials take the same branches.  Only the order k_shadow visits nodes in changes.
+static_assert(BKT_N == 64, "k_extend's last wave flushes one bucket per lane");
+__device__ __forceinline__ int bucket_key(const WArgs &W, int bucket) {  // counter of (bucket, this block's slice)
+    return bucket * BKT_S + (int)(blockIdx.x % BKT_S);
+}
+
 // Closest hit (World.cast, world.js:28-30).  Chain: ray q of the batch; tree: level L's range.
 template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L, double minD) {
+    __shared__ uint32_t hist[BKT_N], waves_done;  // bucketed hand-off: the block's lit hits per bucket
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     uint32_t i = t;
     bool live = true;
@@ -445,17 +437,19 @@ __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs
     } else {
         const LevelRange R = level_range(W, L);
         if (t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // the launch bound was too small
-        if (W.bucket) {  // every thread reaches block_claim below
+        if (!W.bucket) {
+            if (t >= R.count) return;
+        } else {  // every wave of a live block reaches the count below
             if (blockIdx.x * 256u >= R.count) return;  // block-uniform
+            if (threadIdx.x < BKT_N) hist[threadIdx.x] = 0u;
+            if (threadIdx.x == 0) waves_done = 0u;
+            __syncthreads();
             live = t < R.count;
-        } else if (t >= R.count) {
-            return;
         }
         i = R.base + (live ? t : 0u);
     }
-    live = live && W.prim[i] != NO_RAY;
     int hp = -1;
-    if (live) {
+    if (live && W.prim[i] != NO_RAY) {
         const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
         const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
         W.t[i] = h.t;
@@ -463,23 +457,42 @@ __global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs
         W.ctx[i] = h.ctx;
         hp = h.prim;
     }
-    if (!CHAIN && W.bucket) (void)block_claim<256>(W.bkt + (size_t)(2 * L) * BKT_N, hp >> (W.bucket - 1), hp >= 0);
+    if (!CHAIN && W.bucket) {
+        // Bucketed hand-off: ranks every lit hit (S.prim_lit: shade_node lights every hit but Solid /
+        // Transparent) among the block's hits in its bucket (wave-aggregated LDS atomics); the
+        // block's last wave adds the histogram to the level's per-key counters (one global atomic per
+        // bucket per block, keys spread over BKT_S slices) and keeps the block's bases.  No barrier
+        // waits for the block's slowest cast, and the atomics overlap other blocks' casts (as a
+        // separate pass they cost cornell 30 ms per frame, r02_s16).
+        const bool lit = hp >= 0 && S.prim_lit[hp] != 0;
+        const int b = lit ? hp >> (W.bucket - 1) : 0;
+        const int lane = (int)__lane_id();
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        uint64_t todo = __ballot(lit);
+        while (todo) {  // one LDS atomic per distinct bucket of the wave (a few hot buckets would serialise)
+            const int first = __builtin_ctzll(todo);
+            const int bv = __shfl(b, first);
+            const uint64_t m = __ballot(lit && b == bv);
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(&hist[bv], (uint32_t)__popcll(m));
+            base = __shfl(base, first);
+            if (lit && b == bv) W.brank[i] = base + (uint32_t)__popcll(m & lt);
+            todo &= ~m;
+        }
+        __threadfence_block();
+        uint32_t done = 0;
+        if (lane == 0) done = atomicAdd(&waves_done, 1u);
+        if (__shfl(done, 0) == 256u / 64u - 1u) {  // the block's last wave: BKT_N == 64 lanes flush
+            __threadfence_block();
+            const uint32_t c = hist[lane];
+            if (c) W.bbase[(size_t)blockIdx.x * BKT_N + lane] = atomicAdd(W.bkt + (size_t)L * BKT_LEVEL + bucket_key(W, lane), c);
+        }
+    }
 }
 
-// Bucketed shadow hand-off (WArgs::bucket = shift + 1): the lit nodes of level L are written grouped
-// by hit primitive (bucket prim >> shift: one primitive each in a flat scene, runs of consecutive
-// triangles in a mesh) -- bucket b starts after the hits of buckets 0..b-1 (counted by k_extend) --
-// so the 64 lanes of a k_shadow wave serve nodes on one surface: their shadow rays cull the same
-// objects and walk the same BVH nodes, and their materials take the same branches.  Only the order
-// k_shadow visits nodes in changes.
-__device__ __forceinline__ int bucket_count(const DScene &S, const WArgs &W) { return ((S.n_prims - 1) >> (W.bucket - 1)) + 1; }
-__device__ __forceinline__ uint32_t bucket_start(const DScene &S, const WArgs &W, int L, int b) {
-    const CONST_AS uint32_t *cnt = as_const(W.bkt + (size_t)(2 * L) * BKT_N);
-    uint32_t off = 0;
-    const int nb = bucket_count(S, W);
-    for (int j = 0; j < nb; ++j) off += j < b ? cnt[j] : 0u;
-    return off;
-}
+// Offsets of the level's hand-off keys: an exclusive prefix over the k_extend counts (key order =
+// bucket-major), and the level's lit-node total.  One block.
+__global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L);
 
 // World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
 // Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
@@ -539,11 +552,11 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         }
         return;
     }
-    if (W.bucket) {  // the lit node's hand-off into its primitive's bucket (see bucket_start)
-        const bool lit = hit && (out.info & INFO_LIT);
-        const int b = lit ? prim >> (W.bucket - 1) : 0;
-        const uint32_t k = block_claim<256>(W.bkt + (size_t)(2 * L + 1) * BKT_N, b, lit);
-        if (lit) store_hand(W, bucket_start(S, W, L, b) + k, out.h);
+    if (W.bucket && hit && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
+        const int b = prim >> (W.bucket - 1);
+        const uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
+        const uint32_t h = B[2 * BKT_K + bucket_key(W, b)] + W.bbase[(size_t)blockIdx.x * BKT_N + b] + W.brank[r];
+        if (h < B[3 * BKT_K]) store_hand(W, h, out.h);  // (always: k_extend counted this node)
     }
     // tree: children append to level L + 1; at depth 0 they are black without a cast
     const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
@@ -655,18 +668,8 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     const uint32_t s = e % G;
     bool in = q < count;
     const float4 *hp = W.hand + (in ? q : 0u);
-    if (!CHAIN && !SERIAL && W.bucket) {  // hand-off slot q: a lit node if its bucket has filled it
-        const CONST_AS uint32_t *cnt = as_const(W.bkt + (size_t)(2 * L) * BKT_N);
-        const CONST_AS uint32_t *fill = as_const(W.bkt + (size_t)(2 * L + 1) * BKT_N);
-        uint32_t off = 0;
-        bool filled = false;
-        const int nb = bucket_count(S, W);
-        for (int j = 0; j < nb; ++j) {
-            const uint32_t c = cnt[j];
-            filled = filled || (q >= off && q < off + fill[j]);
-            off += c;
-        }
-        in = in && filled;
+    if (!CHAIN && !SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
+        in = q < as_const(W.bkt + (size_t)L * BKT_LEVEL)[3 * BKT_K];
         q = in ? f2u(hp[6 * W.hstride].y) : 0u;
     }
     const uint32_t i = base + (in ? q : 0u);
@@ -837,7 +840,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
     // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
     const bool Q = (PF & PF_SDF) && W.sstride != 0;
     if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
-    if (!CHAIN && W.bucket) (void)hipMemsetAsync(W.bkt, 0, (size_t)MAX_TREE_DEPTH * 2 * BKT_N * sizeof(uint32_t), st);
+    if (!CHAIN && W.bucket) (void)hipMemsetAsync(W.bkt, 0, (size_t)MAX_TREE_DEPTH * BKT_LEVEL * sizeof(uint32_t), st);
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
     std::vector<size_t> ubs;  // launch bound of each level's ray count
     for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
@@ -851,6 +854,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
             else
                 hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
+        if (!CHAIN && W.bucket) hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(256), 0, st, W, L);
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
         });

@@ -942,6 +942,10 @@ struct Loader {
         }
         shading_matrices();
         leaf_triangles();
+        for (const DPrim &pr : S.prims) {  // shade_node: every material but Solid / Transparent takes light samples
+            const uint32_t k = S.mat[pr.material].kind;
+            S.prim_lit.push_back(k != JSRT_MAT_SOLID && k != JSRT_MAT_TRANSPARENT ? 1 : 0);
+        }
         S.profile = f == 0 ? PF_ANALYTIC : (f & ~PF_MESH) == 0 ? PF_MESH : (f & ~PF_SDF) == 0 ? PF_SDF : PF_ALL;
         for (uint32_t i = 0; i < B.n_sdf; ++i) S.sdf_nodes.push_back(B.sdf[i]);
         if (B.n_sdf) S.sdf_child.assign(B.chld, B.chld + B.n_chld);

@@ -12,6 +12,7 @@ namespace jsrt {
 struct HostScene {
     std::vector<DPrim> prims;
     std::vector<int32_t> prim_obj;     // per DPrim: its OBJS index in the blob (jsrt_cast)
+    std::vector<int32_t> prim_lit;     // per DPrim: its material takes light samples (DScene::prim_lit)
     std::vector<DInst> insts;
     std::vector<int32_t> inst_child, roots;
     std::vector<RootBound> rbounds;
