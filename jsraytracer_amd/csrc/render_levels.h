@@ -27,6 +27,9 @@
 #ifndef JSRT_EXTEND_OCC
 #define JSRT_EXTEND_OCC 5
 #endif
+#ifndef JSRT_EXTEND_OCC_FLAT  // analytic profile: 6 fits without spills (cornell +1 %, r02_s20)
+#define JSRT_EXTEND_OCC_FLAT 6
+#endif
 // optional waves-per-EU window (min, max) per kernel for A/B occupancy experiments
 #ifdef JSRT_SHADOW_WPE
 #define SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(JSRT_SHADOW_WPE)))
@@ -427,7 +430,8 @@ __device__ __forceinline__ int bucket_key(const WArgs &W, int bucket) {  // coun
 
 // Closest hit (World.cast, world.js:28-30).  Chain: ray q of the batch; tree: level L's range.
 template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256, JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L, double minD) {
+__global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSRT_EXTEND_OCC) void k_extend(DScene S, WArgs W, int L,
+                                                                                                 double minD) {
     __shared__ uint32_t hist[BKT_N], waves_done;  // bucketed hand-off: the block's lit hits per bucket
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     uint32_t i = t;
