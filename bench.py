@@ -26,7 +26,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including:
                    duration against 8 TB/s.
   cpu_baseline  -- the C oracle (port of the reference path) on a bounded column subsample, host cores,
                    with the reference JS web-worker figure recorded in BASELINE.md beside it.
-  parity        -- the timed frame's columns checked against the oracle's render of the same columns:
+  parity        -- the last timed frame's columns checked against the oracle's render of the same columns:
                    RGBA8 bit-exact, f32 colour |d| <= 1e-5 (north_star), at the benchmark's full size.
 """
 import argparse
@@ -301,16 +301,22 @@ def main():
         st_full = step(0 if w == max(args.warmup, 1) - 1 else None)
     dom = max(st_full["stage_ms"], key=lambda k: st_full["stage_ms"][k])
     # timed region: HIP events bracket only the dominant kernel's launches (its average launch
-    # duration for the roofline); events on every launch would add launch gaps to the step
+    # duration for the roofline); events on every launch would add launch gaps to the step.  The last
+    # timed step also writes the f32 colours handed to setColor (k_final, 16 B per pixel): the parity
+    # block checks that frame itself.
+    colors = torch.empty(fg.maxcols * H * 4, dtype=torch.float32, device=f"cuda:{local}") if world == 1 else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step(None if args.no_events else (1 << STAGES.index(dom))) for _ in range(args.steps)]
+    stats = [step(None if args.no_events else (1 << STAGES.index(dom)), colors if k == args.steps - 1 else None)
+             for k in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_image = FrameGather.to_rgba8(fg.image).copy() if rank == 0 else None  # the last timed frame
+    timed_cols = colors.view(fg.maxcols, H, 4)[:W].permute(1, 0, 2).cpu().numpy() if colors is not None else None
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host_tiles else f"cuda:{local}")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -319,10 +325,8 @@ def main():
         stats = [step(1 << STAGES.index(dom))]
     dom_ms = sum(s["stage_ms"][dom] for s in stats) / len(stats)
     dom_launches = stats[0]["stage_launches"][dom]
-    # per-stage split: one more step after the timed region with every launch bracketed; at N = 1 it
-    # also returns the f32 colours for the parity check (the same frame: the render is deterministic)
-    colors = torch.empty(fg.maxcols * H * 4, dtype=torch.float32, device=f"cuda:{local}") if world == 1 else None
-    st_after = step(0, colors)
+    # per-stage split: one more step after the timed region with every launch bracketed
+    st_after = step(0)
     stage_ms, stage_launches, kernel_ms = st_after["stage_ms"], st_after["stage_launches"], st_after["kernel_ms"]
     torch.cuda.synchronize()
 
@@ -346,11 +350,9 @@ def main():
                 dx = W // 4 + 17
                 ocol, orgba, _, _ = oracle_columns(blob, W, H, spp, kind, depth, 5, dx, threads)
                 ref = (ocol, orgba, 5, dx)
-            image = FrameGather.to_rgba8(fg.image)
-            cols = None
-            if colors is not None:  # world 1, col_block 1: owned column c is image column c
-                cols = colors.view(fg.maxcols, H, 4)[:W].permute(1, 0, 2).cpu().numpy()
-            par = parity(image, cols, ref)
+            # the last timed frame (world 1, col_block 1: owned column c is image column c)
+            par = parity(timed_image, timed_cols, ref)
+            par["frame"] = "last timed step"
         roof = roofline(args.config, bound, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp)
         size = f"{W}²" if W == H else f"{W}x{H}"
         line = {

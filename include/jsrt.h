@@ -14,6 +14,9 @@
  *   jsrt_render_device  <- same, device-resident outputs on a caller stream (multi-GPU tile path)
  *   jsrt_cast           <- World.cast (src/world.js:28-30) for a batch of rays: closest-hit distance
  *                          and the hit Primitive (known-answer tests localise parity to one cast)
+ *   jsrt_material_data  <- World.color(ray, 1) up to Material.color (world.js:31-41, 125-137):
+ *                          Geometry.materialData + the world normal / position of each hit
+ *   jsrt_sdf_distance   <- SDF.distance (src/sdf.js:53-74) of an SDFGeometry primitive's root
  *   jsrt_scene_destroy  <- worker teardown (src/raytrace_launcher.js:106-124 terminate)
  *   jsrt_last_error     <- the reference throws strings (e.g. src/aggregates.js:39); errors here are
  *                          negative return codes + this message, never C++ exceptions.
@@ -58,7 +61,7 @@ typedef struct {
     uint32_t launches;       /* render-kernel launches */
     uint32_t batches;        /* (pixels x samples) batches of the wavefront schedule */
     double stage_ms[JSRT_STAGES];        /* per kernel: gen, extend, shade, shadow, reduce, accum, final,
-                                            resolve, trace (extend+shade+shadow fused), 3 spare */
+                                            resolve, 4 spare */
     uint32_t stage_launches[JSRT_STAGES];
     uint32_t attempts;       /* frame attempts: > 1 when a pool / launch bound was outgrown and the frame redone */
     uint32_t events_lost;    /* event pairs whose elapsed time HIP could not report (not in stage_ms) */
@@ -93,6 +96,19 @@ int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col
  * for none.  Synchronous. */
 int jsrt_cast(jsrt_scene *scene, const float *rays, size_t n, double min_dist, double max_dist,
               int32_t intersect_transparent, double *out_dist, int32_t *out_object);
+
+/* World.color(ray, 1) up to Material.color (world.js:31-41, 125-137) of n rays (as jsrt_cast): the
+ * closest hit of World.cast(ray, 0) -- out_dist, out_object as jsrt_cast -- and the material_data the
+ * hit Primitive hands to its material: normal (n x 4 f32: inv_transform.transposed().times(n).to4(0)
+ * .normalized()), position (n x 4: ray.getPoint(distance)), uv (n x 3: UV, the third component always
+ * NaN), bary (n x 3: a triangle's barycentric coordinates), basecolor (n x 3: an SDF's); NaN where a
+ * field is absent (or no hit).  Synchronous. */
+int jsrt_material_data(jsrt_scene *scene, const float *rays, size_t n, double *out_dist, int32_t *out_object,
+                       float *normal, float *position, float *uv, float *bary, float *basecolor);
+
+/* SDF.distance (sdf.js:53-74) of the root SDF of SDFGeometry primitive `object` (its OBJS index in the
+ * blob) at n points (f32 x 4 in the primitive's local frame, w = 1).  Synchronous. */
+int jsrt_sdf_distance(jsrt_scene *scene, int32_t object, const float *points, size_t n, double *out);
 
 /* Number of owned columns for (W, x_offset, x_delt, col_block). */
 int32_t jsrt_owned_columns(int32_t width, int32_t x_offset, int32_t x_delt, int32_t col_block);

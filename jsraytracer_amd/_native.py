@@ -9,6 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JSRT_LIB") or os.path.join(HERE, "_build", "libjsrt.so")  # JSRT_LIB: A/B builds
+ABI_VERSION = 2  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
 
 
 class JsrtError(RuntimeError):
@@ -23,7 +24,7 @@ class Params(ctypes.Structure):
                 ("max_paths", ctypes.c_int32), ("stage_events", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
-STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve", "k_trace",
+STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve", "spare8",
           "spare9", "spare10", "spare11"]
 NSTAGES = len(STAGES)  # JSRT_STAGES
 
@@ -45,7 +46,8 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_v
 
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_cast",
-           "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version", "jsrt_device_count"]
+           "jsrt_material_data", "jsrt_sdf_distance", "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version",
+           "jsrt_device_count"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 # exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
@@ -96,6 +98,10 @@ def lib():
     L.jsrt_cast.restype = ctypes.c_int
     L.jsrt_cast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double, ctypes.c_double,
                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+    L.jsrt_material_data.restype = ctypes.c_int
+    L.jsrt_material_data.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_void_p] * 7
+    L.jsrt_sdf_distance.restype = ctypes.c_int
+    L.jsrt_sdf_distance.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     L.jsrt_owned_columns.restype = ctypes.c_int32
     L.jsrt_owned_columns.argtypes = [ctypes.c_int32] * 4
     L.jsrt_last_error.restype = ctypes.c_char_p
@@ -116,6 +122,9 @@ def lib():
                                       ctypes.POINTER(JsonInfo)]
     L.jsrt_blob_free.restype = None
     L.jsrt_blob_free.argtypes = [ctypes.c_void_p]
+    # a stale library (the .so travels to the GPU box on its own) would write past Stats or misread it
+    if L.jsrt_abi_version() != ABI_VERSION:
+        raise JsrtError(f"{LIB_PATH}: ABI {L.jsrt_abi_version()}, these bindings expect {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 

@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libjsrt.so")
 PROFILES = {"analytic": 0, "mesh": 9, "sdf": 4, "all": 15}  # device_scene.h PF_ANALYTIC / PF_MESH / PF_SDF / PF_ALL
-HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "render_levels.h", "scene_load.h",
+HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "render_levels.h", "scene_load.h", "sdf_forms.h",
            "sdf_program.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")
@@ -34,6 +34,10 @@ UNITS += [("capi", "capi.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
           ("mesh_build", "mesh_build.cpp", [], ["jsrt_mesh.h", "jsrt_scene.h", "obj_parse.h"]),
           ("json_scene", "json_scene.cpp", [], ["jsrt_json.h", "jsrt_scene.h", "obj_parse.h"])]
 OBJ_FLAGS = [f for f in FLAGS if f != "-shared"]
+# No machine-level loop-invariant code motion: it hoists address and f64-constant materialisations out
+# of the light-sample and traversal loops into VGPRs and then spills them (k_shade_lit: 66 spilled
+# VGPRs at 128; k_extend 80 -> 74 VGPRs without it).  -DJSRT_MACHINE_LICM (a variant define) keeps it.
+NO_MLICM = ["-mllvm", "-disable-machine-licm"]
 
 
 def _path(f):
@@ -57,6 +61,8 @@ def _deps(src, deps):
 
 def _stale():
     objs = [_obj(stem) for stem, _, _, _ in UNITS]
+    if os.path.exists(LIB) and not any(os.path.exists(o) for o in objs):
+        return False  # a prebuilt library shipped without its objects (the GPU box's snapshot): use it
     return any(_newer(_obj(stem), _deps(src, deps)) for stem, src, _, deps in UNITS) or _newer(LIB, objs)
 
 
@@ -85,8 +91,9 @@ def _build_locked(force, verbose, variant, defines, profiles):
         o = _obj(stem, tag if mine else "")
         objs.append(o)
         if force or mine or _newer(o, _deps(src, deps)):
-            cmd = [HIPCC] + OBJ_FLAGS + defs + (list(defines) if mine else []) + ["-c", os.path.join(CSRC, src),
-                                                                                 "-o", o + ".tmp"]
+            extra = list(defines) if mine else []
+            dev = [] if "-DJSRT_MACHINE_LICM" in extra or not src.endswith(".hip") else NO_MLICM
+            cmd = [HIPCC] + OBJ_FLAGS + dev + defs + extra + ["-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
             jobs.append((cmd, o))
 
     def run(job):

@@ -260,12 +260,14 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     std::vector<uint32_t> h_prev;
     std::function<bool(int, double, bool)> prog;
     int prev_rc = 0;
+    bool reported = false;  // a callback (or preview) has reached the caller: a retry would repeat passes
     if (progress && tl > 0)
         prog = [&](int pass, double completion, bool clean) {  // renderers.js:103-112 cadence, batch granularity
             if (completion >= 1.0) return true;
             auto now = std::chrono::steady_clock::now();
             if (std::chrono::duration<double, std::milli>(now - t_last).count() >= tl) {
                 t_last = now;
+                reported = true;
                 if (preview && clean) {
                     const size_t npx = (size_t)a.ncols * a.H;
                     h_prev.resize(npx);
@@ -290,6 +292,11 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     // wavefront_bytes_per_path: ~1.8 KB per path on the tree schedule, 60 GB at 32 M paths): the
     // default is capped at half the device memory free now, and a batch whose buffers cannot be
     // allocated is retried at half the size (the batch size never changes a bit of the image).
+    // Simple / RandomMultisampling with a callback report per batch (renderers.js:28-37): at least 8
+    if (prog && a.kind != JSRT_RENDERER_INCREMENTAL) {
+        const size_t work = (size_t)a.patches * 64 * (size_t)a.spp;
+        max_paths = std::min(max_paths, std::max<size_t>(64, (work + 7) / 8));
+    }
     if (!(p && p->max_paths > 0)) {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
@@ -303,7 +310,9 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
     hipError_t e;
     for (;;) {
         e = render_frame(s->ds, a, s->ns, *wf, stream, st ? &kt : nullptr, max_paths, prog);
-        if (e != hipErrorOutOfMemory || max_paths <= ((size_t)1 << 16)) break;
+        // out of device memory: retry at half the batch, unless a callback already saw part of this
+        // frame (its passes / completion would repeat or go backwards)
+        if (e != hipErrorOutOfMemory || max_paths <= ((size_t)1 << 16) || reported) break;
         (void)hipGetLastError();
         max_paths /= 2;
         wf->release();
@@ -368,6 +377,63 @@ int jsrt_cast(jsrt_scene *s, const float *rays, size_t n, double min_dist, doubl
         const int32_t p = out_object[i];
         out_object[i] = (p >= 0 && (size_t)p < po.size()) ? po[p] : -1;
     }
+    return 0;
+}
+
+int jsrt_material_data(jsrt_scene *s, const float *rays, size_t n, double *out_dist, int32_t *out_object, float *normal,
+                       float *position, float *uv, float *bary, float *basecolor) {
+    if (!s) return set_error(-1, "scene is NULL");
+    if (n == 0) return 0;
+    if (!rays || !out_dist || !out_object || !normal || !position || !uv || !bary || !basecolor)
+        return set_error(-1, "NULL buffer");
+    if (n > (size_t)UINT32_MAX / 16) return set_error(-1, "too many rays");
+    HIP_TRY(hipSetDevice(s->device));
+    // one device buffer: rays (6 f32), t (f64), prim (i32), normal + position (8 f32), uv + bary + basecolor (9 f32)
+    const size_t o_t = (n * 6 * 4 + 7) & ~(size_t)7, o_p = o_t + n * 8, o_f = o_p + n * 4, total = o_f + n * 17 * 4;
+    uint8_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, total);
+    float *f = reinterpret_cast<float *>(d + o_f);
+    if (e == hipSuccess) e = hipMemcpy(d, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = material_data_rays(s->ds, reinterpret_cast<const float *>(d), (uint32_t)n, reinterpret_cast<double *>(d + o_t),
+                               reinterpret_cast<int32_t *>(d + o_p), f, f + 4 * n, f + 8 * n, f + 11 * n, f + 14 * n, 0);
+    std::vector<float> h(n * 17);
+    if (e == hipSuccess) e = hipMemcpy(out_dist, d + o_t, n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_object, d + o_p, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), f, n * 17 * 4, hipMemcpyDeviceToHost);
+    if (d) (void)hipFree(d);
+    if (e != hipSuccess) return set_error(-3, std::string("jsrt_material_data: ") + hipGetErrorString(e));
+    memcpy(normal, h.data(), n * 16);
+    memcpy(position, h.data() + 4 * n, n * 16);
+    memcpy(uv, h.data() + 8 * n, n * 12);
+    memcpy(bary, h.data() + 11 * n, n * 12);
+    memcpy(basecolor, h.data() + 14 * n, n * 12);
+    const std::vector<int32_t> &po = s->hs.prim_obj;
+    for (size_t i = 0; i < n; ++i) {
+        const int32_t p = out_object[i];
+        out_object[i] = (p >= 0 && (size_t)p < po.size()) ? po[p] : -1;
+    }
+    return 0;
+}
+
+int jsrt_sdf_distance(jsrt_scene *s, int32_t object, const float *points, size_t n, double *out) {
+    if (!s) return set_error(-1, "scene is NULL");
+    int32_t g = -1;
+    for (size_t p = 0; p < s->hs.prims.size(); ++p)
+        if (s->hs.prim_obj[p] == object && s->hs.prims[p].gkind == JSRT_GEOM_SDF) g = s->hs.prims[p].gindex;
+    if (g < 0) return set_error(-1, "object " + std::to_string(object) + " is not an SDFGeometry primitive");
+    if (n == 0) return 0;
+    if (!points || !out) return set_error(-1, "NULL buffer");
+    if (n > (size_t)UINT32_MAX / 16) return set_error(-1, "too many points");
+    HIP_TRY(hipSetDevice(s->device));
+    uint8_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, n * 16 + n * 8);
+    if (e == hipSuccess) e = hipMemcpy(d, points, n * 16, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = sdf_distance_points(s->ds, g, reinterpret_cast<const float *>(d), (uint32_t)n, reinterpret_cast<double *>(d + n * 16), 0);
+    if (e == hipSuccess) e = hipMemcpy(out, d + n * 16, n * 8, hipMemcpyDeviceToHost);
+    if (d) (void)hipFree(d);
+    if (e != hipSuccess) return set_error(-3, std::string("jsrt_sdf_distance: ") + hipGetErrorString(e));
     return 0;
 }
 

@@ -40,13 +40,34 @@ JSRT_HD double js_sign(double x) {
     if (is_nan(x) || x == 0.0) return x;
     return x > 0 ? 1.0 : -1.0;
 }
+// (ah + al) * (bh + bl) in double-double (Dekker / fma two-product): relative error ~2^-104
+__device__ __forceinline__ void dd_mul(double ah, double al, double bh, double bl, double &rh, double &rl) {
+    const double p = ah * bh;
+    const double e = fma(ah, bh, -p) + (ah * bl + al * bh);
+    rh = p + e;
+    rl = e - (rh - p);
+}
+// x^n, integer 1 <= n <= 64, 0 <= x <= 2, by binary powering in double-double and one final rounding:
+// the correctly rounded power except for a value within ~2^-100 relative of a rounding boundary (libm's
+// f64 pow -- V8's fdlibm, glibc, OCML -- is itself only within ~1 ulp there).  A third of the VALU
+// of OCML's general pow for the Phong exponents the reference scenes use (10, 100).
+__device__ __forceinline__ double pow_int_dd(double x, int n) {
+    double bh = x, bl = 0.0, rh = 1.0, rl = 0.0;
+    for (;;) {
+        if (n & 1) dd_mul(rh, rl, bh, bl, rh, rl);
+        n >>= 1;
+        if (!n) break;
+        dd_mul(bh, bl, bh, bl, bh, bl);
+    }
+    return rh + rl;
+}
 __device__ __forceinline__ double js_pow(double x, double y) {
-#ifdef JSRT_AB_NOPOW  // A/B timing only: not the reference's arithmetic
-    return x * y;
-#endif
     if (is_nan(y)) return __builtin_nan("");
     if (y == 0.0) return 1.0;
     if ((x == 1.0 || x == -1.0) && __builtin_isinf(y)) return __builtin_nan("");
+#ifndef JSRT_LIBM_POW
+    if (x >= 0.0 && x <= 2.0 && y >= 1.0 && y <= 64.0 && y == floor(y)) return pow_int_dd(x, (int)y);
+#endif
     return pow(x, y);
 }
 __device__ __forceinline__ double js_round(double x) {  // Math.round (half toward +inf)
@@ -306,24 +327,27 @@ struct RegFile {  // per-lane doubles addressed by a wave-uniform index
     }
 };
 
+#include "sdf_forms.h"
+
 __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P) {
     RegFile<SDF_MAX_D> dst;
     RegFile<SDF_MAX_S> sst;
     F3 pst0 = P, pst1 = P;  // SDF_MAX_P == 2
     int lc0 = 0, lc1 = 0;   // SDF_MAX_LOOP == 2
     int dsp = 0, psp = 0, ssp = 0, lsp = 0;
-#ifndef JSRT_AB_FLAT_VM
     // The program and its constants are read-only and every index is wave-uniform: through the
     // constant address space the loads are scalar (s_load, scalar cache) instead of a vector load per
     // lane on the interpreter's dependent chain.
     const CONST_AS SdfInsn *code = as_const(S.sdf_insn);
     const CONST_AS double *K = as_const(S.sdf_const);
-#else
-    const SdfInsn *code = S.sdf_insn;
-    const double *K = S.sdf_const;
-#endif
     pc = uni(pc);  // uniform among the active lanes (sdf_node_dist's waterfall)
     end = uni(end);
+    if (uni(code[pc].op) == SOP_FORM) {  // a recognised shape: straight-line code (sdf_forms.h)
+        const int form = uni(code[pc].a);
+        if (form == SFORM_RUNION_DIFF) return sdf_form_runion_diff(K, code, pc + 1, P);
+        if (form == SFORM_RUNION) return sdf_form_runion(K, code, pc + 1, P);
+        ++pc;  // (unknown form: the VM runs its instructions)
+    }
     while (pc < end) {
         const int op = uni(code[pc].op), ia = uni(code[pc].a), ib = uni(code[pc].b);
         switch (op) {
@@ -575,8 +599,6 @@ __device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
     return res;
 }
 
-#include "prim_filter.h"
-
 // --------------------------------------------------------------------------------------------
 // world intersection (world.js:7-15, 116-124; aggregates.js:14-18, 43-49, 207-225)
 struct Hit {
@@ -584,10 +606,6 @@ struct Hit {
     int prim;
     int ctx;
 };
-
-#ifdef JSRT_DBG_COUNT  // A/B instrumentation only: per-object lane / wave test counts of world_cast
-__device__ unsigned long long g_dbg[256];
-#endif
 
 template <int PF>
 __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DPrim &P, F3 o, F3 d, double minD,
@@ -758,36 +776,6 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
     }
 }
 
-// The f32 pre-test of a top-level primitive (prim_filter.h) for the caller's (minD, lim): FLT_EXACT
-// for the kinds without one (cylinder, triangle, SDF) and for non-primitive roots.
-// Which kinds get a pre-test (bit 0 planar, 1 AABB, 2 sphere) and whether closest-hit casts use it
-// (ANY casts always do).  Off by default: A/B on MI355X (cornell) -- the top-level
-// loop is wave-uniform, so a pre-test costs every wave that needs the object its full instruction
-// count, and the exact forms (early-out after the plane distance, f64 divisions) are no dearer:
-// no pre-test 406.6 M/s, AABB 404.0, AABB + sphere 398.9, all kinds 376.8, + closest-hit 374.3.
-#ifndef JSRT_FILTER_KINDS
-#define JSRT_FILTER_KINDS 0
-#endif
-#ifndef JSRT_FILTER_CLOSEST
-#define JSRT_FILTER_CLOSEST 0
-#endif
-template <bool ANY>
-__device__ __forceinline__ bool root_filtered(int k) {
-    if (!ANY && !JSRT_FILTER_CLOSEST) return false;
-    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) return (JSRT_FILTER_KINDS & 1) != 0;
-    if (k == JSRT_GEOM_AABB) return (JSRT_FILTER_KINDS & 2) != 0;
-    if (k == JSRT_GEOM_SPHERE) return (JSRT_FILTER_KINDS & 4) != 0;
-    return false;
-}
-__device__ __forceinline__ int root_filter(const DRoot &R, F3 o, F3 d, float oabs, float dabs, const FBounds &B) {
-    const int k = R.p.gkind;
-    const FRows &F = R.fr;
-    const FRay Y = fray(F, o, d, oabs, dabs);
-    if (k == JSRT_GEOM_AABB) return aabb_filter(F, R.p.center, R.p.half, Y, B);
-    if (k == JSRT_GEOM_SPHERE) return sphere_filter(F, Y, B);
-    return planar_filter(k, F, Y, B);
-}
-
 // Conservative cull of one top-level object: false only when the object provably
 // cannot produce an accepted hit on the segment (minD, flim): the ray misses its world box inflated
 // by k|o| + e0 (flim = (float) of the far limit min(best, maxD)).
@@ -821,51 +809,21 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     Hit best{DINF, -1, 0};
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    const float dabs = fmaxf(fabsf(d.x), fmaxf(fabsf(d.y), fabsf(d.z)));
     const float fminD = (float)minD;
-    FBounds FB = fbounds(minD, maxD, maxD);  // the pre-tests' (minD, lim), lim = min(maxD, best)
     bool live = true;
-#ifdef JSRT_DBG_COUNT
-    const uint64_t act0 = __ballot(1);
-    if (__lane_id() == __builtin_ctzll(act0)) {
-        atomicAdd(&g_dbg[(ANY ? 192 : 128) + 62], (unsigned long long)__popcll(act0));
-        atomicAdd(&g_dbg[(ANY ? 192 : 128) + 63], 1ull);
-    }
-#endif
     float flim = (float)maxD;  // (float)min(best, maxD): the cull's far limit, updated with best
     for (int i = 0; i < S.n_roots; ++i) {
         const DRoot &R = S.rootrec[i];
         const bool need = live && root_needed(R.rb, o, ix, iy, iz, oabs, fminD, flim);
         if (!__any(need)) continue;
-#ifdef JSRT_DBG_COUNT
-        {
-          const uint64_t act = __ballot(1), nb = __ballot(need);
-          if (__lane_id() == __builtin_ctzll(act)) {
-            atomicAdd(&g_dbg[(ANY ? 192 : 128) + 2 * i], (unsigned long long)__popcll(nb));
-            atomicAdd(&g_dbg[(ANY ? 192 : 128) + 2 * i + 1], 1ull);
-          }
-        }
-#endif
         if (!need) {  // (a divergent if, not a divergent continue: the loop itself stays uniform)
         } else if (R.kind == INST_PRIM) {
-            // f32 pre-test first: the exact f64 test runs only for decisions too close to call
-            const double lim = fmin(maxD, best.t);
-            int f = FLT_EXACT;
-            if (!transp && !R.p.casts_shadow) f = FLT_NO;
-            else if (root_filtered<ANY>(R.p.gkind)) f = root_filter(R, o, d, oabs, dabs, FB);
-#ifdef JSRT_DBG_COUNT
-            atomicAdd(&g_dbg[100 + (ANY ? 4 : 0) + f + 1], 1ull);
-#endif
-            if (f == FLT_NO) {
-            } else if (ANY && f == FLT_YES) {  // an accepted hit; any-hit callers read only 0 < t < 1
-                best = Hit{0.5 * (minD + lim), R.prim, 0};
-                live = false;
-            } else {
-                const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, lim);
+            // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
+            if (transp || R.p.casts_shadow) {
+                const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
                 if (t > minD && t < best.t && t < maxD) {
                     best = Hit{t, R.prim, 0};
                     flim = (float)best.t;
-                    if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, best.t);
                     if (ANY) live = false;
                 }
             }
@@ -875,13 +833,11 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;
                 flim = (float)best.t;
-                if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, best.t);
                 if (ANY) live = false;
             }
         } else if (PF & PF_AGG) {
             nested_cast<PF, ANY>(S, R.inst, o, d, minD, maxD, transp, best);
             flim = (float)(best.t < maxD ? best.t : maxD);
-            if (!ANY && JSRT_FILTER_CLOSEST) FB = fbounds(minD, maxD, fmin(maxD, best.t));
             if (ANY && best.prim >= 0) live = false;
         }
     }
@@ -1020,12 +976,10 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
 // --------------------------------------------------------------------------------------------
 // materials (materials.js)
 __device__ __forceinline__ F3 mc_eval(const DScene &S, int m, float u, float v) {  // MaterialColor.color(data)
-#ifndef JSRT_AB_MC_WALK
     {  // a chain that does not read (u, v): its colour, computed by the loader (scene_load.cpp mc_constants)
         const float4 cc = *reinterpret_cast<const float4 *>(S.mc_const + 4 * m);
         if (cc.w != 0.0f) return f3(cc.x, cc.y, cc.z);
     }
-#endif
     // walk Scaled* wrappers (and checkerboard choices) down to the solid colour, then apply the
     // scales innermost first: ScaledMaterialColor.color = child.color(data).times(scale)
     auto step = [&](int x) {  // next record below x (checkerboards resolved by (u, v))
@@ -1101,7 +1055,9 @@ __device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, 
 
 // One sample of lights.js sampleIterator for `Lt` seen from world point P: the direction (delta, NOT
 // normalised: the shadow ray's t in (1e-4, 1) spans the segment) and the sample colour.
-__device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, F3 P, Rng &rng, F3 &delta, F3 &L,
+// LT: DLight in any address space (a wave-uniform record is read through the constant one: scalar loads)
+template <class LT>
+__device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P, Rng &rng, F3 &delta, F3 &L,
                                              F3 &lcol) {
     if (Lt.kind == JSRT_LIGHT_POINT) {  // SimplePointLight.sampleIterator (lights.js:45-53)
         delta = sub(f3(Lt.pos[0], Lt.pos[1], Lt.pos[2]), P);
@@ -1121,7 +1077,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, 
             const double b = rng.next() - 0.5;
             local = f3((float)a, (float)b, 0.0f);
         }
-        const double *T = Lt.T;
+        const auto *T = Lt.T;
         const F3 wpos = f3((float)((((double)local.x * T[0] + (double)local.y * T[1]) + (double)local.z * T[2]) + T[3]),
                            (float)((((double)local.x * T[4] + (double)local.y * T[5]) + (double)local.z * T[6]) + T[7]),
                            (float)((((double)local.x * T[8] + (double)local.y * T[9]) + (double)local.z * T[10]) + T[11]));
@@ -1134,7 +1090,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const DLight &Lt, 
             float nw = 1.0f;
             if (nn > 0.00001) { n = scale(local, 1 / nn); nw = (float)(1.0 * (1 / nn)); }
             cart_to_sph(n, u, v);
-            const double *Ti = Lt.Ti;  // inv_transform.transposed().times(n).to4(0).normalized()
+            const auto *Ti = Lt.Ti;  // inv_transform.transposed().times(n).to4(0).normalized()
             const float wx = (float)((((double)n.x * Ti[0] + (double)n.y * Ti[4]) + (double)n.z * Ti[8]) + (double)nw * Ti[12]);
             const float wy = (float)((((double)n.x * Ti[1] + (double)n.y * Ti[5]) + (double)n.z * Ti[9]) + (double)nw * Ti[13]);
             const float wz = (float)((((double)n.x * Ti[2] + (double)n.y * Ti[6]) + (double)n.z * Ti[10]) + (double)nw * Ti[14]);
@@ -1163,15 +1119,9 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
     if (probSum == 0) return false;
     if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
         const double theta = 2.0 * JS_PI * rng.next();
-#ifdef JSRT_AB_NOTRIG  // A/B timing only: not the reference's arithmetic
-        const double phi = 2.0 * rng.next() - 1.0;
-        const double sin_phi = phi * 0.5;
-        const F3 sp3 = f3((float)(theta * sin_phi), or0((float)phi), or0((float)(theta * 0.1 * sin_phi)));
-#else
         const double phi = acos(2.0 * rng.next() - 1.0);
         const double sin_phi = sin(phi);
         const F3 sp3 = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
-#endif
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;

@@ -60,52 +60,6 @@ struct RootBound {       // conservative world-space bound of one top-level obje
 };
 static_assert(sizeof(RootBound) == 48, "RootBound");
 
-// The f32 view of a primitive's inverse transform for the pre-tests (prim_filter.h): the 3x3 part
-// rounded to f32, the world position T = -A^-1 m3 (f32), the residual c_r = m_r . T + m_r3 (f64,
-// rounded to f32), per row rn = |m0| + |m1| + |m2| rounded up, and the absolute term of the f64
-// evaluations (the reference's Mat x Vec and c_r): ga = 2^-48 max rn, gb = 2^-48 (max |m3| + max |T| max rn).
-struct FRows {
-    float m[9];
-    float T[3];
-    float c[3];
-    float rn[3];
-    float ga, gb;
-};
-static_assert(sizeof(FRows) == 80, "FRows");
-
-inline void frows_build(const double *inv, FRows &R) {  // host: scene_load.cpp, tests/native
-    const double *a = inv;
-    const double det = a[0] * (a[5] * a[10] - a[6] * a[9]) - a[1] * (a[4] * a[10] - a[6] * a[8]) +
-                       a[2] * (a[4] * a[9] - a[5] * a[8]);
-    double T[3] = {0, 0, 0};
-    if (det != 0 && std::isfinite(det)) {  // T = -A^-1 m3 (Cramer); any T is valid, this one makes c ~ 0
-        const double b[3] = {-a[3], -a[7], -a[11]};
-        T[0] = (b[0] * (a[5] * a[10] - a[6] * a[9]) - a[1] * (b[1] * a[10] - a[6] * b[2]) + a[2] * (b[1] * a[9] - a[5] * b[2])) / det;
-        T[1] = (a[0] * (b[1] * a[10] - a[6] * b[2]) - b[0] * (a[4] * a[10] - a[6] * a[8]) + a[2] * (a[4] * b[2] - b[1] * a[8])) / det;
-        T[2] = (a[0] * (a[5] * b[2] - b[1] * a[9]) - a[1] * (a[4] * b[2] - b[1] * a[8]) + b[0] * (a[4] * a[9] - a[5] * a[8])) / det;
-        for (double &t : T)
-            if (!std::isfinite(t)) t = 0;
-    }
-    double rnmax = 0, m3max = 0, tmax = 0;
-    for (int r = 0; r < 3; ++r) {
-        const float Tf = (float)T[r];
-        R.T[r] = std::isfinite(Tf) ? Tf : 0.0f;
-    }
-    for (int r = 0; r < 3; ++r) {
-        const double *m = inv + 4 * r;
-        for (int k = 0; k < 3; ++k) R.m[3 * r + k] = (float)m[k];
-        R.c[r] = (float)(m[0] * R.T[0] + m[1] * R.T[1] + m[2] * R.T[2] + m[3]);
-        const double n = fabs(m[0]) + fabs(m[1]) + fabs(m[2]);
-        R.rn[r] = nextafterf((float)(n * (1 + 1e-12)), INFINITY);
-        rnmax = fmax(rnmax, n);
-        m3max = fmax(m3max, fabs(m[3]));
-        tmax = fmax(tmax, fabs((double)R.T[r]));
-    }
-    const double g = 3.552713678800501e-15;  // 2^-48
-    R.ga = nextafterf((float)(g * rnmax * 1.01), INFINITY);
-    R.gb = nextafterf((float)(g * (m3max + tmax * rnmax) * 1.01), INFINITY);
-}
-
 struct DRoot {           // one top-level object flattened for the world loop: every field the cull
     RootBound rb;        // and the test read sits in one record, read through independent scalar loads
     int32_t kind;        // INST_*
@@ -113,9 +67,8 @@ struct DRoot {           // one top-level object flattened for the world loop: e
     int32_t prim;        // INST_PRIM: DPrim index (p is its copy); else -1
     int32_t pad;
     DPrim p;             // INST_PRIM: the primitive; AGG/BVH: p.inv = the object's inverse matrix
-    FRows fr;            // the f32 view of p.inv for the pre-tests
 };
-static_assert(sizeof(DRoot) == 288, "DRoot");
+static_assert(sizeof(DRoot) == 208, "DRoot");
 
 struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
     float cx, cy, cz;

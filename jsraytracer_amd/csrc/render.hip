@@ -24,7 +24,7 @@
 namespace jsrt {
 
 const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final",
-                                    "k_resolve", "k_trace"};
+                                    "k_resolve"};
 
 // camera rays: one per path q of the batch, sample-major (neighbouring q are neighbouring pixels)
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
@@ -73,15 +73,23 @@ __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
     if (tt >= R.count) return;
     const uint32_t i = R.base + tt;
     const float4 nd = W.node[i];
+    const uint32_t p = W.parent[i];  // issued with the node record, not after the child loads
     const uint32_t info = f2u(nd.w);
-    if (!(info & INFO_HIT)) return;
+    if (!(info & INFO_HIT) || p == DEAD_RAY) return;
     F3 c = f3(nd.x, nd.y, nd.z);
     const int n = (int)((info >> INFO_NCHILD_SHIFT) & 3);
     for (int j = 0; j < n; ++j) {
         const float4 v = W.slot[(size_t)j * W.nstride + i];
         c = add_child(W, i, (uint32_t)j, c, f3(v.x, v.y, v.z));
     }
-    write_result(W, i, c);
+    if (p == NO_PARENT) {  // write_result
+        float *dst = W.root + 3 * (size_t)W.path[i];
+        dst[0] = c.x;
+        dst[1] = c.y;
+        dst[2] = c.z;
+    } else {
+        W.slot[(size_t)(p & 1u) * W.nstride + (p >> 1)] = make_float4(c.x, c.y, c.z, 0.0f);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L) {
@@ -267,7 +275,8 @@ size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
     if (S.max_children <= 1)  // chain: one ray and depth nodes per path
         return ray + (size_t)std::max(1, max_depth) * node + hand + (persist ? group * 48 : 0);
     const size_t pool = 8, level_cap = pool / 2;  // render_frame: pool = 8 x paths, level_cap = pool / 2
-    return pool * (ray + 8 + node + 2 * 16) + level_cap * (hand + (persist ? group * 48 : 0)) + 12;
+    // + the bucketed hand-off's ranks (4 B per pool slot) and block bases (BKT_N words per 256 hand-off slots)
+    return pool * (ray + 8 + node + 2 * 16 + 4) + level_cap * (hand + (persist ? group * 48 : 0) + BKT_N * 4 / 256) + 12;
 }
 
 
@@ -322,6 +331,42 @@ JSRT_CAST_EXTERN(PF_MESH)
 JSRT_CAST_EXTERN(PF_SDF)
 JSRT_CAST_EXTERN(PF_ALL)
 #undef JSRT_CAST_EXTERN
+
+#define JSRT_MD_EXTERN(PFV)                                                                                          \
+    extern template void material_data_pf<PFV>(const DScene &, const float *, uint32_t, double *, int32_t *, float *, \
+                                               float *, float *, float *, float *, hipStream_t);
+JSRT_MD_EXTERN(PF_ANALYTIC)
+JSRT_MD_EXTERN(PF_MESH)
+JSRT_MD_EXTERN(PF_SDF)
+JSRT_MD_EXTERN(PF_ALL)
+#undef JSRT_MD_EXTERN
+
+hipError_t material_data_rays(const DScene &S, const float *d_rays, uint32_t n, double *d_t, int32_t *d_prim,
+                              float *d_nrm, float *d_pos, float *d_uv, float *d_bary, float *d_bc, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    switch (S.profile) {
+    case PF_ANALYTIC: material_data_pf<PF_ANALYTIC>(S, d_rays, n, d_t, d_prim, d_nrm, d_pos, d_uv, d_bary, d_bc, st); break;
+    case PF_MESH: material_data_pf<PF_MESH>(S, d_rays, n, d_t, d_prim, d_nrm, d_pos, d_uv, d_bary, d_bc, st); break;
+    case PF_SDF: material_data_pf<PF_SDF>(S, d_rays, n, d_t, d_prim, d_nrm, d_pos, d_uv, d_bary, d_bc, st); break;
+    default: material_data_pf<PF_ALL>(S, d_rays, n, d_t, d_prim, d_nrm, d_pos, d_uv, d_bary, d_bc, st); break;
+    }
+    return hipGetLastError();
+}
+
+// SDF.distance of SDF geometry g's root (sdf.js:53-74) at points (f32 x 4, w = 1): the same program VM
+// the render's march runs (jsrt_sdf_distance)
+__global__ __launch_bounds__(256) void k_sdf_distance(DScene S, int g, const float *pts, uint32_t n, double *out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float *p = pts + 4 * (size_t)i;
+    out[i] = sdf_node_dist(S, S.sdfg[g].root, f3(p[0], p[1], p[2]));
+}
+
+hipError_t sdf_distance_points(const DScene &S, int g, const float *d_pts, uint32_t n, double *d_out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sdf_distance, dim3(grid_ub(n)), dim3(256), 0, st, S, g, d_pts, n, d_out);
+    return hipGetLastError();
+}
 
 hipError_t cast_rays(const DScene &S, const float *d_rays, uint32_t n, double min_dist, double max_dist, bool transparent,
                      double *d_t, int32_t *d_prim, hipStream_t st) {
@@ -382,6 +427,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree schedule)
     if (!chain && (e = hipHostMalloc((void **)&h_lvl, 64 * sizeof(uint32_t), 0)) != hipSuccess) return e;
     bool conservative = false;
+    double reported = 0;  // completion already reported: a redone frame reports only beyond it
     for (int attempt = 0; e == hipSuccess; ++attempt) {
         if (kt) kt->attempts = (uint32_t)attempt + 1;
         const size_t pool = chain ? paths : paths * wf.pool_factor, level_cap = chain ? paths : pool / 2;
@@ -438,6 +484,18 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 if ((e = hipGetLastError()) != hipSuccess) break;
                 done += (uint64_t)W.npix * nb;
                 if (kt) ++kt->batches;
+                if (progress && A.kind != JSRT_RENDERER_INCREMENTAL) {
+                    // Simple / RandomMultisampling report {pass: 0, completion: pixels done / total} from
+                    // inside their pixel loop (renderers.js:28-37): here after every batch
+                    if (!chain && (e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+                    const bool clean = chain || (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]);
+                    const double c = (double)done / (double)total;
+                    if (c > reported) {
+                        reported = c;
+                        if ((stop = !progress(0, c, clean))) break;
+                    }
+                }
                 if (!chain && ((wf.frac.empty() && !conservative) || conservative)) {
                     // learn the level counts: from the scene's first batch, or -- when that batch was
                     // not representative and a frame had to be redone -- as the maximum over every
@@ -451,11 +509,15 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     }
                 }
             }
-            if (e == hipSuccess && progress) {  // completion of finished work: wait for the pass
+            if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL) {  // completion of finished work: wait for the pass
                 if (!chain && (e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
                 if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
                 const bool clean = chain || (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]);
-                stop = !progress((int)(s0 + nb - 1), (double)done / (double)total, clean);
+                const double c = (double)done / (double)total;
+                if (c > reported) {
+                    reported = c;
+                    stop = !progress((int)(s0 + nb - 1), c, clean);
+                }
             }
         }
         if (e != hipSuccess || chain) break;

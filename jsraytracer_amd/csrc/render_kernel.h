@@ -94,7 +94,7 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     ~Wavefront();
 };
 
-enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_TRACE, KT_N };
+enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_N };
 extern const char *const KT_NAMES[KT_N];
 
 struct EventPairs {  // reusable HIP events bracketing every launch of one kernel kind
@@ -138,6 +138,14 @@ hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st);
 // w = 0): closest-hit distance and DPrim index (-1: none).  The jsrt_cast entry (known-answer tests).
 hipError_t cast_rays(const DScene &S, const float *d_rays, uint32_t n, double min_dist, double max_dist, bool transparent,
                      double *d_t, int32_t *d_prim, hipStream_t st);
+
+// World.color(ray, 1) up to Material.color for n rays (jsrt_material_data): closest hit of World.cast(ray,
+// 0) and the hit's material_data -- world normal (n x 4), world position (n x 4), UV (n x 3), triangle
+// barycentric coordinates (n x 3), SDF basecolor (n x 3), NaN where absent.
+hipError_t material_data_rays(const DScene &S, const float *d_rays, uint32_t n, double *d_t, int32_t *d_prim,
+                              float *d_nrm, float *d_pos, float *d_uv, float *d_bary, float *d_bc, hipStream_t st);
+// SDF.distance of SDF geometry g's root at n local points (f32 x 4) (jsrt_sdf_distance).
+hipError_t sdf_distance_points(const DScene &S, int g, const float *d_pts, uint32_t n, double *d_out, hipStream_t st);
 
 // Owned column c -> image column px (see jsrt.h jsrt_render_device).
 __host__ __device__ inline int32_t owned_to_px(int32_t c, int32_t x_offset, int32_t x_delt, int32_t col_block) {

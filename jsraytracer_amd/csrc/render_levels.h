@@ -73,6 +73,57 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
+// Block-aggregated append with the block's children grouped by a 3-bit key (the direction octant): one
+// atomic per block on the level counter; o0 / o1 = the offsets of this thread's children in the block's
+// range (children of one key contiguous, in no particular order within a key).  Every thread of the
+// block must call it.
+__device__ __forceinline__ uint32_t block_append_keyed(uint32_t *counter, int n, int k0, int k1, uint32_t &o0,
+                                                       uint32_t &o1) {
+    __shared__ uint32_t s_cnt[8], s_base[9];
+    if (threadIdx.x < 8) s_cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const int lane = (int)__lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t r[2] = {0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bool has = n > j;
+        const int k = j == 0 ? k0 : k1;
+        uint64_t todo = __ballot(has);
+        while (todo) {  // one LDS atomic per distinct key of the wave
+            const int first = __builtin_ctzll(todo);
+            const int kv = __builtin_amdgcn_readlane(k, first);
+            const uint64_t m = __ballot(has && k == kv);
+            uint32_t b = 0;
+            if (lane == first) b = atomicAdd(&s_cnt[kv], (uint32_t)__popcll(m));
+            b = __shfl(b, first);
+            if (has && k == kv) r[j] = b + (uint32_t)__popcll(m & lt);
+            todo &= ~m;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < 8; ++k) {
+            s_base[k] = acc;
+            acc += s_cnt[k];
+        }
+        s_base[8] = acc ? atomicAdd(counter, acc) : 0u;
+    }
+    __syncthreads();
+    o0 = s_base[k0 & 7] + r[0];
+    o1 = s_base[k1 & 7] + r[1];
+    return s_base[8];
+}
+__device__ __forceinline__ int octant(F3 d) { return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0); }
+
+// A block's children are appended grouped by direction octant (k_shade), so a wave of the next level's
+// k_extend casts rays of one or two octants: they cull the same objects and walk the same BVH subtrees.
+// A/B on MI355X (profiles/r03_s2_ab.txt): bunny +5.5 % (k_extend 27.9 -> 25.5 ms), cornell +-0.
+#ifndef JSRT_CHILD_SORT
+#define JSRT_CHILD_SORT 1
+#endif
+
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
     if (p == DEAD_RAY) return;
@@ -129,12 +180,19 @@ struct NodeOut {
     Handoff h;      // h.pos (the hit point) is set for every hit; the rest for lit nodes
 };
 
-// World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
-// Geometry.materialData + Material.color (materials.js).  Fills the node (info, ambient / surface,
-// shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
-template <int PF>
-__device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
-                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1) {
+// Primitive.color (world.js:125-137) up to Material.color: Geometry.materialData of the hit (per kind,
+// geometry.js / sdf.js:41-47) and the world normal inv_transform.transposed().times(n).to4(0)
+// .normalized().  ALL (the material-data known answers, jsrt_material_data): UV of every kind that has
+// one and a triangle's barycentric coordinates, whether or not the material reads them.
+struct Surface {
+    F3 N;          // world normal (w = 0)
+    float u, v;    // UV (when has_uv, or when the material reads it)
+    F3 basecolor;  // SDF basecolor, else (1, 1, 1)
+    F3 bary;       // ALL: a triangle's barycentric coordinates
+    int has_uv, has_bc, has_bary;
+};
+template <int PF, bool ALL>
+__device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o, F3 d, bool need_uv, Surface &sf) {
     const DPrim &P = S.prims[h.prim];
     // inv_transform = prim.inv x ancestorInvTransform (float64, math.js:399-409); the host
     // precomputed it (same operations) for identity prims and for the top-level context
@@ -162,13 +220,15 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
                 }
         }
     }
-    const bool need_uv = (S.mat_flags[P.material] & MATF_UV) != 0;
+    if (ALL) need_uv = true;
     const F3 lo = xf_point(inv, o), ld = xf_dir(inv, d);
     const F3 pl = ray_point(lo, ld, h.t);  // base_data.position (local)
     F3 nrm = f3(0, 0, 0);
     float nrm_w = 0.0f;
     float u = 0, v = 0;
     F3 basecolor = f3(1, 1, 1);
+    int has_uv = 0, has_bc = 0, has_bary = 0;
+    F3 bary = f3(0, 0, 0);
     switch (P.gkind) {
     case JSRT_GEOM_PLANE:
     case JSRT_GEOM_SQUARE:
@@ -176,6 +236,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         nrm = f3(0, 0, 1);
         u = pl.x;
         v = pl.y;
+        has_uv = 1;
         break;
     case JSRT_GEOM_SPHERE: {  // geometry.js:449-455: position.normalized() includes w = 1
         const double nn = sqrt(dot3(pl, pl) + 1.0);
@@ -183,6 +244,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         nrm_w = 1.0f;
         if (nn > 0.00001) { nrm = scale(pl, 1 / nn); nrm_w = (float)(1.0 * (1 / nn)); }
         if (need_uv) cart_to_sph(nrm, u, v);
+        has_uv = 1;
         break;
     }
     case JSRT_GEOM_CYLINDER:  // geometry.js:479-487
@@ -191,6 +253,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
             u = (float)(0.5 + atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
             v = (float)(0.5 + (double)pl.z);
         }
+        has_uv = 1;
         break;
     case JSRT_GEOM_AABB: {  // geometry.js:210-224
         double norm_dist = 0;
@@ -213,21 +276,26 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         if (!(PF & PF_TRI)) break;
         const DTri &T = S.tris[P.gindex];
         nrm = f3(T.n[0], T.n[1], T.n[2]);
-        if (T.shade >= 0) {
-            const DTriShade &TS = S.trish[T.shade];
+        if (ALL || T.shade >= 0) {  // toBarycentric (geometry.js:389-396)
             const F3 v2 = f3(pl.x - T.p0[0], pl.y - T.p0[1], pl.z - T.p0[2]);
             const double d20 = dot3(v2, f3(T.v0[0], T.v0[1], T.v0[2])), d21 = dot3(v2, f3(T.v1[0], T.v1[1], T.v1[2]));
             const double bv = (T.d11 * d20 - T.d01 * d21) / T.denom, bw = (T.d00 * d21 - T.d01 * d20) / T.denom;
             const float b0 = (float)(1 - bv - bw), b1 = (float)bv, b2 = (float)bw;
-            if (TS.has_uv) {
-                u = (TS.uv[0][0] * b0 + TS.uv[1][0] * b1) + TS.uv[2][0] * b2;
-                v = (TS.uv[0][1] * b0 + TS.uv[1][1] * b1) + TS.uv[2][1] * b2;
-            }
-            if (TS.has_normal) {
-                nrm = f3((TS.vn[0][0] * b0 + TS.vn[1][0] * b1) + TS.vn[2][0] * b2,
-                         (TS.vn[0][1] * b0 + TS.vn[1][1] * b1) + TS.vn[2][1] * b2,
-                         (TS.vn[0][2] * b0 + TS.vn[1][2] * b1) + TS.vn[2][2] * b2);
-                nrm_w = (TS.vn[0][3] * b0 + TS.vn[1][3] * b1) + TS.vn[2][3] * b2;
+            bary = f3(b0, b1, b2);
+            has_bary = 1;
+            if (T.shade >= 0) {  // Triangle.blend of the psdata (geometry.js:397-409)
+                const DTriShade &TS = S.trish[T.shade];
+                if (TS.has_uv) {
+                    u = (TS.uv[0][0] * b0 + TS.uv[1][0] * b1) + TS.uv[2][0] * b2;
+                    v = (TS.uv[0][1] * b0 + TS.uv[1][1] * b1) + TS.uv[2][1] * b2;
+                    has_uv = 1;
+                }
+                if (TS.has_normal) {
+                    nrm = f3((TS.vn[0][0] * b0 + TS.vn[1][0] * b1) + TS.vn[2][0] * b2,
+                             (TS.vn[0][1] * b0 + TS.vn[1][1] * b1) + TS.vn[2][1] * b2,
+                             (TS.vn[0][2] * b0 + TS.vn[1][2] * b1) + TS.vn[2][2] * b2);
+                    nrm_w = (TS.vn[0][3] * b0 + TS.vn[1][3] * b1) + TS.vn[2][3] * b2;
+                }
             }
         }
         break;
@@ -241,21 +309,40 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         const float ny = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + step, pl.z + 0.0f)) - dist0) / G.normal_step);
         const float nz = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + 0.0f, pl.z + step)) - dist0) / G.normal_step);
         const SdfMD md = sdf_material(S, G.root, pl);
-        if (md.has_bc) basecolor = md.bc;
-        if (md.has_uv) { u = md.u; v = md.v; }
+        if (md.has_bc) { basecolor = md.bc; has_bc = 1; }
+        if (md.has_uv) { u = md.u; v = md.v; has_uv = 1; }
         nrm = normalized(f3(nx, ny, nz));
         break;
     }
     default: break;
     }
     // normal = inv_transform.transposed().times(normal).to4(0).normalized()  (world.js:133-134)
-    F3 N;
     {
         const float wx = (float)((((double)nrm.x * inv[0] + (double)nrm.y * inv[4]) + (double)nrm.z * inv[8]) + (double)nrm_w * inv[12]);
         const float wy = (float)((((double)nrm.x * inv[1] + (double)nrm.y * inv[5]) + (double)nrm.z * inv[9]) + (double)nrm_w * inv[13]);
         const float wz = (float)((((double)nrm.x * inv[2] + (double)nrm.y * inv[6]) + (double)nrm.z * inv[10]) + (double)nrm_w * inv[14]);
-        N = normalized(f3(wx, or0(wy), or0(wz)));
+        sf.N = normalized(f3(wx, or0(wy), or0(wz)));
     }
+    sf.u = u;
+    sf.v = v;
+    sf.basecolor = basecolor;
+    sf.bary = bary;
+    sf.has_uv = has_uv;
+    sf.has_bc = has_bc;
+    sf.has_bary = has_bary;
+}
+
+// World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
+// Geometry.materialData + Material.color (materials.js).  Fills the node (info, ambient / surface,
+// shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
+template <int PF>
+__device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
+                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1) {
+    const DPrim &P = S.prims[h.prim];
+    Surface sf;
+    surface_data<PF, false>(S, h, o, d, (S.mat_flags[P.material] & MATF_UV) != 0, sf);
+    const F3 N = sf.N, basecolor = sf.basecolor;
+    const float u = sf.u, v = sf.v;
     ShadeData sd;
     sd.pos = ray_point(o, d, h.t);  // material_data.position = ray.getPoint(distance)
     out.h.pos = sd.pos;
@@ -424,6 +511,10 @@ inline unsigned grid_ub(size_t n) { return (unsigned)std::max<size_t>(1, (n + 25
 // one surface: their shadow rays cull the same objects and walk the same BVH nodes, and their
 // materials take the same branches.  Only the order k_shadow visits nodes in changes.
 static_assert(BKT_N == 64, "k_extend's last wave flushes one bucket per lane");
+// The bucketed hand-off (and the block appends' 64-bit ballots) assume 64-lane waves (gfx950).
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "the wavefront renderer needs wave64 (build for gfx950)"
+#endif
 __device__ __forceinline__ int bucket_key(const WArgs &W, int bucket) {  // counter of (bucket, this block's slice)
     return bucket * BKT_S + (int)(blockIdx.x % BKT_S);
 }
@@ -521,32 +612,68 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
     int nchild = 0;
     Child ch0, ch1;
     NodeOut out;
-    bool hit = false;
     const int prim = in ? W.prim[r] : NO_RAY;
+    const bool hit = prim >= 0;
+    // Every load, and the children's append (a returning atomic), is issued before the node's first
+    // store: vmcnt counts stores too, in issue order, so a load or atomic issued behind the node's
+    // ~20 HBM stores would wait for all of them to complete.
+    uint32_t parent = 0, path = 0, hslot = ~0u;
+    if (!CHAIN && prim != NO_RAY) {
+        parent = W.parent[r];
+        path = W.path[r];
+    }
+    if (hit) {
+        const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
+        const Hit h{W.t[r], prim, W.ctx[r]};
+        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
+        out.h.node = q;
+        if (!CHAIN && W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
+            const int b = prim >> (W.bucket - 1);
+            const uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
+            hslot = B[2 * BKT_K + bucket_key(W, b)] + W.bbase[(size_t)blockIdx.x * BKT_N + b] + W.brank[r];
+            if (hslot >= B[3 * BKT_K]) hslot = ~0u;  // (never: k_extend counted this node)
+        }
+    }
+    // tree: children append to level L + 1; at depth 0 they are black without a cast
+    uint32_t co[2] = {0u, 1u};  // offsets of the children from `at`
+#if JSRT_CHILD_SORT
+    const uint32_t at = CHAIN ? 0u : block_append_keyed(W.lvl + L + 1, child_depth > 0 ? nchild : 0,
+                                                        nchild > 0 ? octant(ch0.dir) : 0, nchild > 1 ? octant(ch1.dir) : 0,
+                                                        co[0], co[1]);
+#else
+    const uint32_t at = CHAIN ? 0u : block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
+#endif
+    // ---- stores ----
     if (prim == NO_RAY) {
         if (in) store_node(W, i, f3(0, 0, 0), 0u);
-    } else if (prim < 0) {  // miss: World.color returns bg_color (world.js:35-36)
+        return;
+    }
+    if (!hit) {  // miss: World.color returns bg_color (world.js:35-36)
         const F3 bg = f3(S.bg[0], S.bg[1], S.bg[2]);
         if (CHAIN) {
             store_node(W, i, bg, INFO_MISS);
             W.prim[r] = NO_RAY;
         } else {
-            write_result(W, i, bg);
+            if (parent == NO_PARENT) {  // write_result with the preloaded parent / path
+                float *dst = W.root + 3 * (size_t)path;
+                dst[0] = bg.x;
+                dst[1] = bg.y;
+                dst[2] = bg.z;
+            } else if (parent != DEAD_RAY) {
+                W.slot[(size_t)(parent & 1u) * W.nstride + (parent >> 1)] = make_float4(bg.x, bg.y, bg.z, 0.0f);
+            }
             store_node(W, i, bg, 0u);
         }
-    } else {
-        hit = true;
-        const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
-        const Hit h{W.t[r], prim, W.ctx[r]};
-        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
-        store_node(W, i, out.surf, out.info);
-        out.h.node = q;
-        if ((out.info & INFO_LIT) && (CHAIN || !W.bucket)) store_hand(W, q, out.h);
-        if (nchild > 0) store_child(W, i, 0, ch0);
-        if (nchild > 1) store_child(W, i, 1, ch1);
+        return;
     }
+    store_node(W, i, out.surf, out.info);
+    if (out.info & INFO_LIT) {
+        if (CHAIN || !W.bucket) store_hand(W, q, out.h);
+        else if (hslot != ~0u) store_hand(W, hslot, out.h);
+    }
+    if (nchild > 0) store_child(W, i, 0, ch0);
+    if (nchild > 1) store_child(W, i, 1, ch1);
     if (CHAIN) {  // the child ray (World.color(child, depth - 1)) takes over slot q
-        if (!hit) return;
         if (child_depth > 0 && nchild > 0) {
             W.ox[r] = out.h.pos.x; W.oy[r] = out.h.pos.y; W.oz[r] = out.h.pos.z;
             W.dx[r] = ch0.dir.x; W.dy[r] = ch0.dir.y; W.dz[r] = ch0.dir.z;
@@ -556,28 +683,20 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         }
         return;
     }
-    if (W.bucket && hit && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
-        const int b = prim >> (W.bucket - 1);
-        const uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
-        const uint32_t h = B[2 * BKT_K + bucket_key(W, b)] + W.bbase[(size_t)blockIdx.x * BKT_N + b] + W.brank[r];
-        if (h < B[3 * BKT_K]) store_hand(W, h, out.h);  // (always: k_extend counted this node)
-    }
-    // tree: children append to level L + 1; at depth 0 they are black without a cast
-    const uint32_t at = block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
-    if (!hit || nchild == 0) return;
+    if (nchild == 0) return;
     if (child_depth == 0) {
         W.slot[i] = make_float4(0, 0, 0, 0);
         if (nchild > 1) W.slot[W.nstride + i] = make_float4(0, 0, 0, 0);
         return;
     }
-    if ((size_t)at + nchild > W.level_cap || (size_t)next_base + at + nchild > W.pool) {
+    const uint32_t last = at + (nchild > 1 ? (co[0] > co[1] ? co[0] : co[1]) : co[0]);
+    if ((size_t)last + 1 > W.level_cap || (size_t)next_base + last + 1 > W.pool) {
         W.lvl[LVL_FLAG] = 1u;  // outgrew the pool: the host redoes the frame with a larger one
         return;
     }
-    const uint32_t path = W.path[r];
     for (int j = 0; j < nchild; ++j) {
         const Child &c = j == 0 ? ch0 : ch1;
-        const uint32_t rr = next_base + at + (uint32_t)j;
+        const uint32_t rr = next_base + at + co[j];
         W.ox[rr] = out.h.pos.x; W.oy[rr] = out.h.pos.y; W.oz[rr] = out.h.pos.z;
         W.dx[rr] = c.dir.x; W.dy[rr] = c.dir.y; W.dz[rr] = c.dir.z;
         W.addr[rr] = mix32(out.h.addr, (uint32_t)j + 1);
@@ -603,7 +722,10 @@ __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *h
     P = f3(h0.x, h0.y, h0.z);
     Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
     F3 L, lcol;
-    light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
+    if (S.n_lights == 1)  // (kernel argument: uniform) the light record through scalar loads
+        light_sample(S, as_const(S.lights)[0], P, rng, delta, L, lcol);
+    else
+        light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
     const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
     ShadeData sd;
     sd.N = f3(h1.x, h1.y, h1.z);
@@ -613,11 +735,7 @@ __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *h
     sd.spec = f3(h5.x, h5.y, h5.z);
     sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
     sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
-#ifdef JSRT_AB_NOCOLOR
-    return lcol;
-#else
     return light_sample_color((int)f2u(h0.w), sd, L, lcol);
-#endif
 }
 
 __device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
@@ -630,11 +748,7 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, si
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
     if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return f3(0, 0, 0);
-#ifdef JSRT_AB_NOCAST
-    const Hit sh{DINF, -1, 0};
-#else
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
-#endif
     if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
     return c;
 }
@@ -824,6 +938,45 @@ void cast_rays_pf(const DScene &S, const float *rays, uint32_t n, double minD, d
                   int32_t *prim, hipStream_t st) {
     const size_t lds = (PF & (PF_BVH | PF_AGG)) ? bvh_lds_bytes(S, 256) : 0;
     hipLaunchKernelGGL((k_cast_rays<PF>), dim3(grid_ub(n)), dim3(256), lds, st, S, rays, n, minD, maxD, transp, t, prim);
+}
+
+// World.color(ray, 1) up to Material.color for a batch of rays (jsrt_material_data, the material-data
+// known answers): the closest hit of World.cast(ray, 0) (world.js:34) and the hit's surface_data.
+// Absent fields are NaN; uv[2] is always NaN (the kernels read u, v only).
+template <int PF>
+__global__ __launch_bounds__(256) void k_material_data(DScene S, const float *rays, uint32_t n, double *out_t,
+                                                       int32_t *out_prim, float *nrm, float *pos, float *uv,
+                                                       float *bary, float *bc) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + 6 * (size_t)i;
+    const F3 o = f3(r[0], r[1], r[2]), d = f3(r[3], r[4], r[5]);
+    const Hit h = world_cast<PF, false>(S, o, d, 0.0, DINF, true);
+    out_t[i] = h.t;
+    out_prim[i] = h.prim;
+    const float nan = __builtin_nanf("");
+    float *N = nrm + 4 * (size_t)i, *P = pos + 4 * (size_t)i, *U = uv + 3 * (size_t)i, *B = bary + 3 * (size_t)i,
+          *C = bc + 3 * (size_t)i;
+    if (h.prim < 0) {
+        for (int k = 0; k < 4; ++k) N[k] = P[k] = nan;
+        for (int k = 0; k < 3; ++k) U[k] = B[k] = C[k] = nan;
+        return;
+    }
+    Surface sf;
+    surface_data<PF, true>(S, h, o, d, true, sf);
+    const F3 p = ray_point(o, d, h.t);  // material_data.position = ray.getPoint(distance)
+    N[0] = sf.N.x; N[1] = sf.N.y; N[2] = sf.N.z; N[3] = 0.0f;
+    P[0] = p.x; P[1] = p.y; P[2] = p.z; P[3] = 1.0f;
+    U[0] = sf.has_uv ? sf.u : nan; U[1] = sf.has_uv ? sf.v : nan; U[2] = nan;
+    B[0] = sf.has_bary ? sf.bary.x : nan; B[1] = sf.has_bary ? sf.bary.y : nan; B[2] = sf.has_bary ? sf.bary.z : nan;
+    C[0] = sf.has_bc ? sf.basecolor.x : nan; C[1] = sf.has_bc ? sf.basecolor.y : nan; C[2] = sf.has_bc ? sf.basecolor.z : nan;
+}
+template <int PF>
+void material_data_pf(const DScene &S, const float *rays, uint32_t n, double *t, int32_t *prim, float *nrm, float *pos,
+                      float *uv, float *bary, float *bc, hipStream_t st) {
+    const size_t lds = (PF & (PF_BVH | PF_AGG)) ? bvh_lds_bytes(S, 256) : 0;
+    hipLaunchKernelGGL((k_material_data<PF>), dim3(grid_ub(n)), dim3(256), lds, st, S, rays, n, t, prim, nrm, pos, uv,
+                       bary, bc);
 }
 
 // Enqueues one batch without a host round trip.  Chain: every level has exactly npaths slots.

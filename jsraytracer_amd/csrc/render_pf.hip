@@ -13,15 +13,6 @@ template void run_batch<JSRT_PF, false>(const DScene &, const RenderArgs &, cons
                                         const std::vector<size_t> &);
 template void cast_rays_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double, double, int, double *, int32_t *,
                                    hipStream_t);
-
-// A/B instrumentation (variant builds with -DJSRT_DBG_COUNT for one profile): the counters live in
-// this profile's code object, so they are read back from here (tools/dbg_counts.py)
-#ifdef JSRT_DBG_COUNT
-extern "C" int jsrt_debug_counters(unsigned long long *out, int n) {
-    if (n > 256) n = 256;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), n * sizeof(unsigned long long)) != hipSuccess) return -1;
-    static const unsigned long long zero[256] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), zero, sizeof zero) == hipSuccess ? 0 : -1;
-}
-#endif
+template void material_data_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double *, int32_t *, float *, float *,
+                                        float *, float *, float *, hipStream_t);
 }  // namespace jsrt

@@ -624,6 +624,34 @@ struct Loader {
         return {fb, (int32_t)S.sdf_insn.size()};
     }
 
+    // Program shapes with straight-line device code (sdf_forms.h): a recognised fused range gets a copy
+    // prefixed by an SOP_FORM marker (the form reads its constants from the copied instructions).
+    std::pair<int32_t, int32_t> match_sdf_forms(int32_t begin, int32_t end) {
+        const SdfInsn *I = S.sdf_insn.data() + begin;
+        const int32_t n = end - begin;
+        static const int32_t runion[] = {SOP_PUSHP, SOP_MINBOX, SOP_TPUSH, SOP_LOOP, SOP_XMATREP, SOP_MINBOX,
+                                         SOP_MULSMIN, SOP_ENDLOOP, SOP_TPOP, SOP_POPP};
+        auto is_runion = [&](int32_t at) {  // the RecursiveTransformUnion shape at [at, at + 10)
+            bool ok = at + 10 <= n;
+            for (int32_t i = 0; ok && i < 10; ++i) ok = I[at + i].op == runion[i];
+            return ok && I[at + 3].b == begin + at + 7 && I[at + 7].a == begin + at + 3;  // LOOP brackets [4, 6]
+        };
+        int32_t form = 0;
+        if (n == 10 && is_runion(0)) form = SFORM_RUNION;
+        else if (n == 13 && I[0].op == SOP_BOX && is_runion(1) && I[11].op == SOP_NEG && I[12].op == SOP_MAX && I[12].a == 2)
+            form = SFORM_RUNION_DIFF;
+        if (!form) return {begin, end};
+        const int32_t fb = (int32_t)S.sdf_insn.size();
+        S.sdf_insn.push_back(SdfInsn{SOP_FORM, form, 0, 0});
+        for (int32_t i = 0; i < n; ++i) {
+            SdfInsn c = S.sdf_insn[begin + i];
+            if (c.op == SOP_LOOP) c.b += fb + 1 - begin;
+            if (c.op == SOP_ENDLOOP) c.a += fb + 1 - begin;
+            S.sdf_insn.push_back(c);
+        }
+        return {fb, (int32_t)S.sdf_insn.size()};
+    }
+
     int32_t sdfg_index(int32_t g) {
         auto it = sdfg_of_blob.find(g);
         if (it != sdfg_of_blob.end()) return it->second;
@@ -862,7 +890,6 @@ struct Loader {
             r.prim = in.kind == INST_PRIM ? in.prim : -1;
             if (in.kind == INST_PRIM) r.p = S.prims[in.prim];
             else memcpy(r.p.inv, &S.mats[12 * (size_t)in.matrix], sizeof r.p.inv);
-            frows_build(r.p.inv, r.fr);  // f32 view of the inverse rows for the pre-tests (prim_filter.h)
             S.rootrec.push_back(r);
         }
         for (uint32_t i = 0; i < B.n_lite; ++i) {
@@ -960,7 +987,9 @@ struct Loader {
         if (!(nf && nf[0] == '1'))
             for (uint32_t n = 0; n < B.n_sdf; ++n) {
                 if (S.sdf_range[2 * n] < 0) continue;
-                const auto fr = fuse_sdf(S.sdf_range[2 * n], S.sdf_range[2 * n + 1]);
+                auto fr = fuse_sdf(S.sdf_range[2 * n], S.sdf_range[2 * n + 1]);
+                const char *nform = getenv("JSRT_SDF_NOFORMS");  // A/B: the VM for every shape
+                if (!(nform && nform[0] == '1')) fr = match_sdf_forms(fr.first, fr.second);
                 S.sdf_range[2 * n] = fr.first;
                 S.sdf_range[2 * n + 1] = fr.second;
             }

@@ -40,6 +40,13 @@ enum SdfOp : int32_t {
     SOP_XMATS,      // TPUSH XMAT TPOP_MUL: P = inv*P, top = top * (1 * scale)
     SOP_XMATREP,    // TPUSH XMATS XREP TPOP_MUL: a = matrix, b = scale, pad = repetition const
     SOP_MULSMIN,    // MULS, MIN 2: d = pop * top-scale; push Math.min(pop, d)
+    // a recognised program shape (scene_load.cpp match_sdf_forms): a = SFORM_*, the shape's fused
+    // instructions follow and are run as straight-line code (sdf_forms.h)
+    SOP_FORM,
+};
+enum SdfForm : int32_t {
+    SFORM_RUNION_DIFF = 1,  // Difference(Box, RecursiveTransformUnion(Union(Box...), Sequence(Matrix, Repetition)))
+    SFORM_RUNION = 2,       // RecursiveTransformUnion(Union(Box...), Sequence(Matrix, Repetition))
 };
 
 struct SdfInsn {

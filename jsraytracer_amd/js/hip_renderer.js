@@ -20,12 +20,27 @@
  */
 const path = require("path");
 
+const ABI_VERSION = 2;  // include/jsrt.h JSRT_ABI_VERSION this wrapper is written against
 let _addon = null;
 function addon() {
     if (_addon) return _addon;
     const p = process.env.JSRT_NODE_ADDON || path.join(__dirname, "..", "_build", "jsrt_node.node");
-    _addon = require(p);  // throws if the addon was not built: there is no JS fallback renderer
+    const a = require(p);  // throws if the addon was not built: there is no JS fallback renderer
+    // a stale libjsrt (the .so travels to the GPU box separately) would misread the stats struct
+    if (a.abiVersion() !== ABI_VERSION) throw `HipRenderer: libjsrt ABI ${a.abiVersion()}, expected ${ABI_VERSION}`;
+    _addon = a;
     return _addon;
+}
+
+/*
+ * The device a worker renders on: worker i of the reference's launcher (src/raytrace_launcher.js:65-101,
+ * which spawns N workers over one CPU) goes to GPU i % deviceCount, so N workers spread over a node's
+ * GPUs round-robin and each renders its interleaved columns (worker.js:30-32) on its own device.
+ * deviceCount defaults to the devices HIP sees (0 without a GPU -> device 0).
+ */
+function deviceForWorker(workerIndex, deviceCount) {
+    const n = deviceCount !== undefined ? deviceCount : addon().deviceCount();
+    return n > 0 ? workerIndex % n : 0;
 }
 
 const KIND = { SimpleRenderer: 0, IncrementalMultisamplingRenderer: 1, RandomMultisamplingRenderer: 2 };
@@ -117,4 +132,4 @@ class NodePixelBuffer {
 // Primitive carries the material and transform loadObjFile would be given).
 function attachObj(blob, objText, opts) { return addon().attachObj(blob, objText, opts || {}); }
 
-module.exports = { HipRenderer, NodePixelBuffer, addon, readHeader, attachObj };
+module.exports = { HipRenderer, NodePixelBuffer, addon, readHeader, attachObj, deviceForWorker, ABI_VERSION };

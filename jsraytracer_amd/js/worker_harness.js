@@ -6,7 +6,8 @@
  *   node worker_harness.js <scene.jsrt[.gz]> <workers> [out.rgba] [width height spp seed]
  *
  * Spawns <workers> worker_threads.  Each gets the reference's message [scenePath, workerIndex,
- * workerCount], renders its interleaved columns (x_offset = workerIndex, x_delt = workerCount) with
+ * workerCount], takes GPU workerIndex % deviceCount (hip_renderer.js deviceForWorker), renders its
+ * interleaved columns (x_offset = workerIndex, x_delt = workerCount) with
  * renderer.render(buffer, 1000, cb, workerIndex, workerCount) and posts [ImageData, workerIndex,
  * stats|null] ... then ["finished", workerIndex, null], exactly the reference protocol.  The main
  * thread composites like raytrace_launcher.js:92-97 (untouched pixels have alpha 0, so overlaying
@@ -15,7 +16,7 @@
 const fs = require("fs");
 const zlib = require("zlib");
 const { Worker, isMainThread, parentPort, workerData } = require("worker_threads");
-const { HipRenderer, NodePixelBuffer } = require("./hip_renderer");
+const { HipRenderer, NodePixelBuffer, deviceForWorker } = require("./hip_renderer");
 
 function loadBlob(p) {
     let b = fs.readFileSync(p);
@@ -27,14 +28,16 @@ if (!isMainThread) {
     parentPort.on("message", (msg) => {
         const [scenePath, workerIndex, workerCount] = msg;
         const o = workerData.overrides || {};
-        const renderer = new HipRenderer(loadBlob(scenePath), o);
+        // worker i on GPU i % deviceCount: the reference's workers spread over the node's GPUs
+        const device = deviceForWorker(workerIndex);
+        const renderer = new HipRenderer(loadBlob(scenePath), Object.assign({}, o, { device }));
         const W = o.width || renderer.width || 600, H = o.height || 600;
         const buffer = new NodePixelBuffer(W, H);
         const t0 = Date.now();
         renderer.render(buffer, 1000, (stats) => parentPort.postMessage([buffer.imgdata, workerIndex, stats]),
                         workerIndex, workerCount);
         parentPort.postMessage([buffer.imgdata, workerIndex, null]);
-        parentPort.postMessage(["finished", workerIndex, { ms: Date.now() - t0, gpu: renderer.stats }]);
+        parentPort.postMessage(["finished", workerIndex, { ms: Date.now() - t0, gpu: renderer.stats, device }]);
         renderer.destroy();
     });
 } else {
@@ -53,7 +56,7 @@ if (!isMainThread) {
         wk.on("error", (e) => { console.error("worker", i, "failed:", e); process.exitCode = 1; });
         wk.on("message", ([img, idx, stats]) => {
             if (img === "finished") {
-                console.error(`worker ${idx} finished in ${stats.ms / 1000} s`);
+                console.error(`worker ${idx} on device ${stats.device} finished in ${stats.ms / 1000} s`);
                 wk.terminate();
                 if (++finished === N && out) fs.writeFileSync(out, Buffer.from(composite.buffer));
                 return;

@@ -64,6 +64,29 @@ class Scene:
                                       t.ctypes.data, obj.ctypes.data), "jsrt_cast")
         return t, obj
 
+    def material_data(self, rays):
+        """World.color(ray, 1) up to Material.color (include/jsrt.h jsrt_material_data): dict of t, obj,
+        normal (n x 4), position (n x 4), uv (n x 3), bary (n x 3), basecolor (n x 3); NaN = absent."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        n = len(rays)
+        out = {"t": np.empty(n, np.float64), "obj": np.empty(n, np.int32)}
+        for k, w in (("normal", 4), ("position", 4), ("uv", 3), ("bary", 3), ("basecolor", 3)):
+            out[k] = np.empty((n, w), np.float32)
+        check(_native.lib().jsrt_material_data(self._h, rays.ctypes.data, n, out["t"].ctypes.data,
+                                               out["obj"].ctypes.data, out["normal"].ctypes.data,
+                                               out["position"].ctypes.data, out["uv"].ctypes.data,
+                                               out["bary"].ctypes.data, out["basecolor"].ctypes.data),
+              "jsrt_material_data")
+        return out
+
+    def sdf_distance(self, obj, points):
+        """SDF.distance of SDFGeometry primitive `obj` (OBJS index) at local points (include/jsrt.h)."""
+        points = np.ascontiguousarray(points, np.float32).reshape(-1, 4)
+        out = np.empty(len(points), np.float64)
+        check(_native.lib().jsrt_sdf_distance(self._h, int(obj), points.ctypes.data, len(points), out.ctypes.data),
+              "jsrt_sdf_distance")
+        return out
+
     def close(self):
         if getattr(self, "_h", None):
             _native.lib().jsrt_scene_destroy(self._h)

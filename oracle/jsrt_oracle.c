@@ -1063,15 +1063,16 @@ static Vec material_color(Ctx *C, int mi, MData *d, int depth) {
     }
 }
 
-/* Primitive.color (world.js:125-137) + Geometry.materialData */
-static Vec primitive_color(Ctx *C, int o, Ray ray, double distance, const Mat *ancInv, int depth) {
-    const jsrt_rec_object *O = &C->S->obj[o];
+/* Primitive.color (world.js:125-137) up to Material.color: Geometry.materialData, the world normal and
+ * the world position.  bary (nullable): a triangle's barycentric coordinates (geometry.js:376-380). */
+static int material_data(Ctx *C, int o, Ray ray, double distance, const Mat *ancInv, MData *dd, Vec *bary_out) {
+    MData d;
     Mat pinv = obj_inv(C, o);
     Mat inv = mat_mul(&pinv, ancInv);
-    MData d;
     memset(&d, 0, sizeof d);
     d.ray = ray;
     d.distance = distance;
+    const jsrt_rec_object *O = &C->S->obj[o];
     Vec pos = ray_point(ray_transformed(&inv, ray), distance);
     const jsrt_rec_geometry *G = &C->S->geom[O->geometry];
     switch (G->kind) {
@@ -1112,6 +1113,7 @@ static Vec primitive_color(Ctx *C, int o, Ray ray, double distance, const Mat *a
         d.has_normal = 1;
         d.normal = vfrom_rec(T->normal, 4);
         Vec bary = tri_bary(T, pos);
+        if (bary_out) *bary_out = bary;
         if (T->has_uv) { /* objloader inserts UV before normal (objloader.js:198-201) */
             Vec u0 = vfrom_rec(T->uv[0], T->uv_len), u1 = vfrom_rec(T->uv[1], T->uv_len), u2 = vfrom_rec(T->uv[2], T->uv_len);
             d.has_uv = 1;
@@ -1139,14 +1141,22 @@ static Vec primitive_color(Ctx *C, int o, Ray ray, double distance, const Mat *a
         d.normal = vnormalized(N);
         break;
     }
-    default: C->err = 1; set_err("unsupported geometry %u", G->kind); return vof3(0, 0, 0);
+    default: C->err = 1; set_err("unsupported geometry %u", G->kind); return -1;
     }
     if (d.has_normal) {
         Mat invT = mat_transposed(&inv);
         d.normal = vnormalized(vto4(mat_vec(&invT, d.normal), 0));
     }
     d.position = ray_point(ray, distance);
-    return material_color(C, O->material, &d, depth);
+    *dd = d;
+    return 0;
+}
+
+/* Primitive.color (world.js:125-137) + Geometry.materialData */
+static Vec primitive_color(Ctx *C, int o, Ray ray, double distance, const Mat *ancInv, int depth) {
+    MData d;
+    if (material_data(C, o, ray, distance, ancInv, &d, NULL)) return vof3(0, 0, 0);
+    return material_color(C, C->S->obj[o].material, &d, depth);
 }
 
 /* World.color (world.js:31-41) with the keyed-RNG frame of keyed_rng.js around it */
@@ -1351,4 +1361,66 @@ int jsrt_oracle_cast(const void *blob, size_t blob_bytes, const float *rays, siz
         return -3;
     }
     return 0;
+}
+
+static void put_vec(float *dst, int width, const Vec *v, int present) {
+    for (int i = 0; i < width; ++i) dst[i] = (present && v && i < v->n) ? v->v[i] : NAN;
+}
+
+int jsrt_oracle_material_data(const void *blob, size_t blob_bytes, const float *rays, size_t n, double *out_t,
+                              int32_t *out_obj, float *normal, float *position, float *uv, float *bary,
+                              float *basecolor) {
+    Scene S;
+    if (parse_scene(blob, blob_bytes, &S)) return -1;
+    Ctx *C = (Ctx *)calloc(1, sizeof(Ctx));
+    if (!C) return -2;
+    C->S = &S;
+    for (size_t i = 0; i < n && !C->err; ++i) {
+        const float *r = rays + 6 * i;
+        Ray ray = {vof4(r[0], r[1], r[2], 1), vof4(r[3], r[4], r[5], 0)};
+        const Hit h = world_cast(C, ray, 0, INFINITY, 1); /* World.color(ray, 1): cast(ray, 0) */
+        out_t[i] = h.distance;
+        out_obj[i] = h.object;
+        MData d;
+        Vec b = vof3(0, 0, 0);
+        int ok = 0, is_tri = 0;
+        memset(&d, 0, sizeof d);
+        if (h.object >= 0) {
+            Mat anc = mat_identity();
+            for (int k = 0; k < h.nanc; ++k) {
+                Mat ai = obj_inv(C, h.anc[k]);
+                anc = mat_mul(&ai, &anc);
+            }
+            ok = material_data(C, h.object, ray, h.distance, &anc, &d, &b) == 0;
+            is_tri = C->S->geom[C->S->obj[h.object].geometry].kind == JSRT_GEOM_TRIANGLE;
+        }
+        put_vec(normal + 4 * i, 4, &d.normal, ok && d.has_normal);
+        put_vec(position + 4 * i, 4, &d.position, ok);
+        put_vec(uv + 3 * i, 3, &d.uv, ok && d.has_uv);
+        put_vec(bary + 3 * i, 3, &b, ok && is_tri);
+        put_vec(basecolor + 3 * i, 3, &d.basecolor, ok && d.has_basecolor);
+    }
+    const int err = C->err;
+    free(C);
+    if (err) return -3;
+    return 0;
+}
+
+int jsrt_oracle_sdf_distance(const void *blob, size_t blob_bytes, int32_t obj, const float *points, size_t n,
+                             double *out) {
+    Scene S;
+    if (parse_scene(blob, blob_bytes, &S)) return -1;
+    if (obj < 0 || (uint32_t)obj >= S.n_obj) { set_err("no such object"); return -1; }
+    const jsrt_rec_geometry *G = &S.geom[S.obj[obj].geometry];
+    if (G->kind != JSRT_GEOM_SDF) { set_err("object %d is not an SDFGeometry primitive", obj); return -1; }
+    Ctx *C = (Ctx *)calloc(1, sizeof(Ctx));
+    if (!C) return -2;
+    C->S = &S;
+    for (size_t i = 0; i < n && !C->err; ++i) {
+        const float *p = points + 4 * i;
+        out[i] = sdf_root_distance(C, &S.sdfg[G->index], vof4(p[0], p[1], p[2], p[3]));
+    }
+    const int err = C->err;
+    free(C);
+    return err ? -3 : 0;
 }

@@ -63,6 +63,12 @@ def lib():
         L.jsrt_oracle_cast.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_void_p]
+        L.jsrt_oracle_material_data.restype = ctypes.c_int
+        L.jsrt_oracle_material_data.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t] + \
+            [ctypes.c_void_p] * 7
+        L.jsrt_oracle_sdf_distance.restype = ctypes.c_int
+        L.jsrt_oracle_sdf_distance.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_void_p,
+                                               ctypes.c_size_t, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -133,6 +139,55 @@ def cast(blob, rays, min_dist=0.0, max_dist=float("inf"), transparent=True):
                           t.ctypes.data, obj.ctypes.data):
         raise RuntimeError(L.jsrt_oracle_last_error().decode())
     return t, obj
+
+
+def material_data(blob, rays):
+    """World.color(ray, 1) up to Material.color (world.js:31-41, 125-137): dict of t (f64), obj (i32),
+    normal (n x 4), position (n x 4), uv (n x 3), bary (n x 3), basecolor (n x 3) f32, NaN = absent."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    n = len(rays)
+    out = {"t": np.empty(n, np.float64), "obj": np.empty(n, np.int32)}
+    for k, w in (("normal", 4), ("position", 4), ("uv", 3), ("bary", 3), ("basecolor", 3)):
+        out[k] = np.empty((n, w), np.float32)
+    L = lib()
+    if L.jsrt_oracle_material_data(bytes(blob), len(blob), rays.ctypes.data, n, out["t"].ctypes.data,
+                                   out["obj"].ctypes.data, out["normal"].ctypes.data, out["position"].ctypes.data,
+                                   out["uv"].ctypes.data, out["bary"].ctypes.data, out["basecolor"].ctypes.data):
+        raise RuntimeError(L.jsrt_oracle_last_error().decode())
+    return out
+
+
+def sdf_distance(blob, obj, points):
+    """SDF.distance (sdf.js:53-74) of SDFGeometry primitive `obj`'s root at local points (n x 4 f32)."""
+    points = np.ascontiguousarray(points, np.float32).reshape(-1, 4)
+    out = np.empty(len(points), np.float64)
+    L = lib()
+    if L.jsrt_oracle_sdf_distance(bytes(blob), len(blob), int(obj), points.ctypes.data, len(points), out.ctypes.data):
+        raise RuntimeError(L.jsrt_oracle_last_error().decode())
+    return out
+
+
+def golden_material(name):
+    """Known answers computed by the reference (oracle/refharness/make_material_kats.js): the material_data
+    of hits ("material": rays, t, obj, normal, position, uv, bary, basecolor) and SDF.distance samples
+    ("sdf": [{obj, points, distance}])."""
+    import base64
+    with gzip.open(os.path.join(GOLDEN, "material", name + ".json.gz"), "rt") as f:
+        d = json.load(f)
+    m = d["material"]
+    shapes = {"rays": (np.float32, 6), "t": (np.float64, 0), "obj": (np.int32, 0), "normal": (np.float32, 4),
+              "position": (np.float32, 4), "uv": (np.float32, 3), "bary": (np.float32, 3), "basecolor": (np.float32, 3)}
+    for k, (dt, w) in shapes.items():
+        a = np.frombuffer(base64.b64decode(m[k]), dt)
+        m[k] = a.reshape(-1, w) if w else a
+    for e in d["sdf"]:
+        e["points"] = np.frombuffer(base64.b64decode(e["points"]), np.float32).reshape(-1, 4)
+        e["distance"] = np.frombuffer(base64.b64decode(e["distance"]), np.float64)
+    return d
+
+
+def golden_material_scenes():
+    return sorted(f[:-len(".json.gz")] for f in os.listdir(os.path.join(GOLDEN, "material")) if f.endswith(".json.gz"))
 
 
 def golden_casts(name):

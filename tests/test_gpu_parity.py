@@ -115,6 +115,23 @@ def test_gpu_progress_callback(jr):
     assert [c for _, c in seen] == sorted(c for _, c in seen)
 
 
+@pytest.mark.parametrize("kind,spp", [(0, 1), (2, 3)])
+def test_gpu_progress_simple_and_random(jr, kind, spp):
+    """renderers.js:28-37: SimpleRenderer / RandomMultisamplingRenderer report {pass: 0, completion:
+    pixels done / total} from inside their pixel loop.  Through HipRenderer with a tiny timelimit they
+    fire at least one callback, pass 0, completion increasing in (0, 1), and the image equals the
+    render without a callback."""
+    sc = _scene(jr, "cornell_box_path")
+    img = jr.PixelBuffer(48, 40)
+    seen = []
+    jr.HipRenderer(sc, samplesPerPixel=spp, maxRecursionDepth=8, kind=kind, seed=3).render(
+        img, 1e-9, lambda p: seen.append((p["pass"], p["completion"])))
+    assert seen and all(p == 0 and 0 < c < 1 for p, c in seen)
+    assert [c for _, c in seen] == sorted(c for _, c in seen)
+    ref, _, _ = sc.render(48, 40, spp, 8, kind, 3, want_colors=False)
+    assert np.array_equal(img.imgdata, ref)
+
+
 @pytest.mark.parametrize("scene,W,H,spp,depth,x_offset,x_delt", [
     ("cornell_box_path", 40, 32, 6, 8, 0, 1),   # chain schedule
     ("cornell_box_path", 40, 32, 4, 8, 1, 3),   # one worker's columns

@@ -161,10 +161,37 @@ def test_node_partition_matches_reference_workers(addon, tmp_path):
         assert np.array_equal(rgba, grgba)
 
 
+def test_device_for_worker_round_robin():
+    """Worker i of N (src/raytrace_launcher.js:65-101) renders on GPU i % deviceCount: 16 workers over an
+    8-GPU node take devices 0..7 twice; without a device (count 0) every worker names device 0."""
+    code = ("const {deviceForWorker}=require('./jsraytracer_amd/js/hip_renderer');"
+            "const m=(n,c)=>Array.from({length:n},(_,i)=>deviceForWorker(i,c));"
+            "console.log(JSON.stringify([m(16,8),m(3,1),m(4,0),m(5,2)]));")
+    r = _node(code)
+    assert r.returncode == 0, r.stderr
+    a, b, c, d = json.loads(r.stdout)
+    assert a == [i % 8 for i in range(16)]
+    assert b == [0, 0, 0] and c == [0, 0, 0, 0] and d == [0, 1, 0, 1, 0]
+
+
+def test_node_wrapper_checks_abi_version(addon, tmp_path):
+    """hip_renderer.js refuses an addon whose libjsrt reports another ABI (a stale .so would misread the
+    stats struct): a stub addon reporting ABI 1 makes the wrapper throw before any scene is created."""
+    stub = tmp_path / "stub_addon.js"
+    stub.write_text("module.exports={abiVersion:()=>1, deviceCount:()=>0};")
+    code = ("const {addon}=require('./jsraytracer_amd/js/hip_renderer');"
+            "try { addon(); console.log('no throw'); } catch (e) { console.log(String(e)); }")
+    r = subprocess.run([NODE, "-e", code], capture_output=True, text=True, timeout=60, cwd=ROOT,
+                       env=dict(os.environ, JSRT_NODE_ADDON=str(stub)))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("HipRenderer: libjsrt ABI 1, expected 2")
+
+
 @pytest.mark.gpu
 def test_node_worker_protocol_composite(addon, tmp_path):
     """worker_harness.js: N worker_threads speaking src/worker.js's protocol, composited like
-    raytrace_launcher.js:92-97, equal the single-renderer image (partition invariance)."""
+    raytrace_launcher.js:92-97, equal the single-renderer image (partition invariance).  Each worker
+    reports the device it took: worker i on GPU i % deviceCount (all on 0 on a one-GPU box)."""
     tag = "cornell_box_path_incremental_32x32_s2_d8_seed5"
     r = pyoracle.golden_index()[tag]
     scene = os.path.join(ROOT, "tests", "golden", "scenes", "cornell_box_path.jsrt.gz")
@@ -176,6 +203,11 @@ def test_node_worker_protocol_composite(addon, tmp_path):
     _, grgba = pyoracle.golden_image(tag, 32, 32)
     assert r["depth"] == 8
     assert np.array_equal(got, grgba)
+    from jsraytracer_amd import _native
+    ndev = _native.lib().jsrt_device_count()
+    import re
+    devs = {int(w): int(d) for w, d in re.findall(r"worker (\d+) on device (\d+) finished", p.stderr)}
+    assert devs == {i: i % ndev for i in range(3)}, p.stderr
 
 
 @pytest.mark.skipif(not os.path.exists("/root/reference/src/math.js"), reason="reference sources absent (GPU box)")

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box: parity tests of one file set + A/B of library variants on one config (+ debug counters).
+# GPU-box: parity tests of one file set + A/B of library variants on one config.
 #   bash tools/gpu_quick.sh CFG "pytest selection" VARIANT...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -11,6 +11,3 @@ if [ -n "$SEL" ]; then
   tail -3 gpurun_out/quick_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 timeout -k 10 600 bash tools/ab_bench.sh $CFG "$@" || exit $?
-if [ -f jsraytracer_amd/_build/libjsrt_dbg.so ]; then
-  JSRT_LIB=$PWD/jsraytracer_amd/_build/libjsrt_dbg.so timeout -k 10 120 python tools/dbg_counts.py $CFG 512 512 16 8 | tail -4
-fi
