@@ -220,6 +220,22 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
         r["pmc_source"] = src
     if bound == "hbm" and "algorithmic" in r:
         r.update(unit="GB/s", peak=HBM_PEAK_GBS, achieved=r["algorithmic"]["GBs"], frac=r["algorithmic"]["frac_of_hbm"])
+        # the BVH and triangles (16 MB for the dragon) are served from L2 / MALL: `frac` counts algorithmic
+        # bytes, not HBM transfers; the physical traffic and the latency figures that bind sit beside it
+        a = r["algorithmic"]
+        r["frac_kind"] = "cache-served algorithmic bytes (SURVEY.md §8(d)), not physical HBM traffic"
+        if per_sample and counts:
+            visits = (counts.get("node_visits", 0) - counts.get("shadow_node_visits", 0)) if dom.startswith("k_extend") \
+                else counts.get("shadow_node_visits", 0)
+            a["node_visits_per_launch"] = visits * samples_per_frame / launches
+            a["node_visits_per_us"] = a["node_visits_per_launch"] / (avg_ms * 1e3)
+        binding = {"resource": "dependent-load latency (BVH node -> child -> triangle chains)"}
+        if "traffic_frac" in r:
+            binding["physical_hbm_frac"] = r["traffic_frac"]
+        if "valu" in r:
+            binding["valu_issue_frac"] = r["valu"]["issue_frac"]
+            binding["lane_utilisation"] = r["valu"]["lane_utilisation"]
+        r["binding"] = binding
     elif bound == "valu" and "valu" in r:
         r.update(unit="TFLOP/s", peak=F64_PEAK_TFLOPS, achieved=r["valu"]["f64_tflops"],
                  frac=r["valu"]["f64_tflops"] / F64_PEAK_TFLOPS)

@@ -160,6 +160,8 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.cam = H.cam;
     memcpy(D.bg, H.bg, sizeof D.bg);
     D.all_roots_prims = H.all_roots_prims;
+    const char *fo = getenv("JSRT_SDF_FO");  // A/B: 0 = the persistent marches keep the VM fallback
+    D.sdf_all_forms = (fo && fo[0] == '0') ? 0 : H.sdf_all_forms;
     D.profile = H.profile;
     sc->ns = (int)H.sample_light.size();
     *out = sc.release();

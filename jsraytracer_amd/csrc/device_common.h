@@ -471,6 +471,25 @@ __device__ __forceinline__ double sdf_node_dist(const DScene &S, int n, F3 p) {
     return r;
 }
 
+// SDF node n's distance when its program is a recognised form (DScene::sdf_all_forms: every geometry
+// root is one): the form's straight-line code only, so a kernel that needs no VM does not carry its
+// register files (the persistent marches: k_extend_q / k_shadow_cast).
+__device__ __forceinline__ double sdf_form_dist(const DScene &S, int n, F3 p) {
+    const CONST_AS SdfInsn *code = as_const(S.sdf_insn);
+    const CONST_AS double *K = as_const(S.sdf_const);
+    const int pc = S.sdf_range[2 * n];
+    double r = 0;
+    for (;;) {  // waterfall over the lanes' nodes (a wave marches one SDF in every reference scene)
+        const int pcu = uni(pc);
+        if (pc == pcu) {
+            const int form = uni(code[pcu].a);
+            r = form == SFORM_RUNION_DIFF ? sdf_form_runion_diff(K, code, pcu + 1, p) : sdf_form_runion(K, code, pcu + 1, p);
+            break;
+        }
+    }
+    return r;
+}
+
 __device__ __forceinline__ double sdf_intersect(const DScene &S, int g, F3 o, F3 d, double minD, double maxD) {  // sdf.js:12-40
     const jsrt_rec_sdfgeom &G = S.sdfg[g];
     double bmin, bmax;
@@ -909,10 +928,11 @@ __device__ __forceinline__ void march_advance(const DScene &S, MarchState &m, do
 }
 
 // One sphere-tracing step of a marching lane (the body of sdf_intersect's loop).
-template <bool ANY>
+template <bool ANY, bool FO>
 __device__ __forceinline__ void march_step(const DScene &S, MarchState &m, double minD, double maxD) {
     const jsrt_rec_sdfgeom &G = S.sdfg[m.g];
-    const double distance = sdf_node_dist(S, G.root, ray_point(m.lo, m.ld, m.t));
+    const F3 p = ray_point(m.lo, m.ld, m.t);
+    const double distance = FO ? sdf_form_dist(S, G.root, p) : sdf_node_dist(S, G.root, p);
     bool end = false, hit = false;
     if (!__builtin_isfinite(distance)) end = true;
     else if (distance <= G.eps) end = hit = true;
@@ -931,8 +951,9 @@ __device__ __forceinline__ void march_step(const DScene &S, MarchState &m, doubl
 }
 
 // The persistent loop.  Src: bool load(uint32_t job, F3 &o, F3 &d) (false: no ray in that slot),
-// void store(uint32_t job, const Hit &h).  Jobs [0, count) are taken from *ctr.
-template <int PF, bool ANY, class Src>
+// void store(uint32_t job, const Hit &h).  Jobs [0, count) are taken from *ctr.  FO: every SDF root
+// of the scene is a recognised form (sdf_form_dist), no stack VM.
+template <int PF, bool ANY, bool FO, class Src>
 __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, uint32_t count, double minD,
                                                 double maxD, bool transp, Src &src) {
     MarchState m;
@@ -969,7 +990,7 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
                 have = false;
             }
         }
-        if (have && m.marching) march_step<ANY>(S, m, minD, maxD);
+        if (have && m.marching) march_step<ANY, FO>(S, m, minD, maxD);
     }
 }
 

@@ -102,6 +102,8 @@ struct DLight {          // lights.js:27 / :56
     int32_t needs_uv;    // colour depends on UV (a checkerboard in its MaterialColor chain)
     int32_t pad2[3];
     double T[16], Ti[16];
+    double inv_n;        // 1 / (samples of an area light, 1 for a point light): colorFromLights' weight
+    double pad3;
 };
 
 struct DCamera {         // cameras.js:18-53
@@ -152,6 +154,8 @@ struct DScene {
     int32_t bvh_stack;       // LDS traversal-stack entries per lane (deepest BVH node + 2; 0: no BVH)
     const DTri *ltris;       // parallel to leaf_prims: the triangle of a fast leaf entry (leaf order)
     const int32_t *prim_lit; // per prim: 1 if its material takes light samples (not Solid / Transparent)
+    int32_t sdf_all_forms;   // every SDF geometry root is a recognised program form (sdf_forms.h)
+    int32_t pad_forms;
 };
 
 // Dynamic LDS of a casting kernel over a scene with BVHs: per lane a traversal stack of bvh_stack

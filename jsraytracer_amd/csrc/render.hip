@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
     const int n = (int)((info >> INFO_NCHILD_SHIFT) & 3);
     for (int j = 0; j < n; ++j) {
         const float4 v = W.slot[(size_t)j * W.nstride + i];
-        c = add_child(W, i, (uint32_t)j, c, f3(v.x, v.y, v.z));
+        c = add_child(W, i, (uint32_t)j, c, f3(v.x, v.y, v.z), info);
     }
     if (p == NO_PARENT) {  // write_result
         float *dst = W.root + 3 * (size_t)W.path[i];
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
                 v = f3(nd.x, nd.y, nd.z);
             } else if (info & INFO_HIT) {
                 F3 col = f3(nd.x, nd.y, nd.z);
-                if ((info >> INFO_NCHILD_SHIFT) & 3) col = add_child(W, i, 0, col, L == A.max_depth - 1 ? f3(0, 0, 0) : v);
+                if ((info >> INFO_NCHILD_SHIFT) & 3) col = add_child(W, i, 0, col, L == A.max_depth - 1 ? f3(0, 0, 0) : v, info);
                 v = col;
             }
         }
@@ -455,6 +455,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         W.bucket = (!chain && !persist && S.n_prims > 0 && ns > 0 && ns <= 64 && !(be && be[0] == '0')) ? shift + 1 : 0;
         W.pool = pool;
         W.level_cap = level_cap;
+        // children grouped by direction octant where the next cast walks a BVH (A/B on MI355X,
+        // profiles/r03_s3_ab.txt: bunny +5.5 %; cornell -0.8 %, its keyed append costing k_shade 3 ms)
+        const char *cs = getenv("JSRT_CHILD_SORT");
+        W.child_sort = cs ? (cs[0] == '1') : ((S.profile & PF_BVH) != 0);
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
         if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
         auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths

@@ -34,6 +34,9 @@ struct RenderArgs {
 
 // node info bits (k_shade -> k_shadow / k_reduce / k_resolve)
 constexpr uint32_t INFO_HIT = 1u, INFO_LIT = 2u, INFO_MISS = 16u;
+// child j's weight is exactly (1, 1, 1) and its k exactly 1: its record's second plane is not stored and
+// ((v * col) * w) * k is v * col bit for bit (x * 1 is exact in f32 and in f64)
+constexpr uint32_t INFO_UNIT0 = 32u, INFO_UNIT1 = 64u;
 constexpr int INFO_NCHILD_SHIFT = 2;
 
 // Device buffers of one batch.  Two schedules share them (render.hip):
@@ -75,6 +78,7 @@ struct WArgs {
     int32_t group;     // lanes per node in k_shadow: a power of two >= ns (<= 64), or 1 (serial)
     int32_t chain;     // schedule
     int32_t bucket;    // tree schedule: 0, or 1 + shift: k_shadow reads lit nodes bucketed by hit primitive >> shift (bkt)
+    int32_t child_sort; // tree schedule: k_shade appends a block's children grouped by direction octant
     size_t pool, level_cap;
     size_t nstride, hstride;  // plane strides of child / slot and of hand
     size_t sstride;           // entries of sray / scol (0: persistent casts not used)

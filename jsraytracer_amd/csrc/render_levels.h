@@ -117,12 +117,6 @@ __device__ __forceinline__ uint32_t block_append_keyed(uint32_t *counter, int n,
 }
 __device__ __forceinline__ int octant(F3 d) { return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0); }
 
-// A block's children are appended grouped by direction octant (k_shade), so a wave of the next level's
-// k_extend casts rays of one or two octants: they cull the same objects and walk the same BVH subtrees.
-// A/B on MI355X (profiles/r03_s2_ab.txt): bunny +5.5 % (k_extend 27.9 -> 25.5 ms), cornell +-0.
-#ifndef JSRT_CHILD_SORT
-#define JSRT_CHILD_SORT 1
-#endif
 
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
@@ -461,15 +455,22 @@ __device__ __forceinline__ uint32_t f2u(float x) { return __float_as_uint(x); }
 __device__ __forceinline__ void store_node(const WArgs &W, uint32_t i, F3 c, uint32_t info) {
     W.node[i] = make_float4(c.x, c.y, c.z, u2f(info));
 }
+__device__ __forceinline__ bool unit_child(const Child &c) {
+    return c.w.x == 1.0f && c.w.y == 1.0f && c.w.z == 1.0f && c.k == 1.0;
+}
 __device__ __forceinline__ void store_child(const WArgs &W, uint32_t i, uint32_t j, const Child &c) {
     float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
     x[0] = make_float4(c.col.x, c.col.y, c.col.z, c.w.x);
-    x[W.nstride] = make_float4(c.w.y, c.w.z, u2f((uint32_t)__double2loint(c.k)), u2f((uint32_t)__double2hiint(c.k)));
+    if (!unit_child(c))
+        x[W.nstride] = make_float4(c.w.y, c.w.z, u2f((uint32_t)__double2loint(c.k)), u2f((uint32_t)__double2hiint(c.k)));
 }
-// ((v * col) * w) * k added to c: surface.plus(child.times(col).times(w).times(k)) (materials.js:277-330)
-__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v) {
+// ((v * col) * w) * k added to c: surface.plus(child.times(col).times(w).times(k)) (materials.js:277-330).
+// info: the node's INFO_* word (INFO_UNIT0 / INFO_UNIT1: w = (1, 1, 1), k = 1, so the product is v * col).
+__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v, uint32_t info) {
     const float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
-    const float4 a = x[0], b = x[W.nstride];
+    const float4 a = x[0];
+    if (info & (j == 0 ? INFO_UNIT0 : INFO_UNIT1)) return add(c, mul(v, f3(a.x, a.y, a.z)));
+    const float4 b = x[W.nstride];
     const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
     return add(c, scale(mul(mul(v, f3(a.x, a.y, a.z)), f3(a.w, b.x, b.y)), k));
 }
@@ -635,14 +636,18 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         }
     }
     // tree: children append to level L + 1; at depth 0 they are black without a cast
+    // W.child_sort: a block's children grouped by direction octant, so a wave of the next level's k_extend
+    // casts rays of one or two octants that walk the same BVH subtrees (WArgs::child_sort)
     uint32_t co[2] = {0u, 1u};  // offsets of the children from `at`
-#if JSRT_CHILD_SORT
-    const uint32_t at = CHAIN ? 0u : block_append_keyed(W.lvl + L + 1, child_depth > 0 ? nchild : 0,
-                                                        nchild > 0 ? octant(ch0.dir) : 0, nchild > 1 ? octant(ch1.dir) : 0,
-                                                        co[0], co[1]);
-#else
-    const uint32_t at = CHAIN ? 0u : block_append<256>(W.lvl + L + 1, child_depth > 0 ? nchild : 0);
-#endif
+    uint32_t at = 0;
+    if (!CHAIN) {
+        const int nc = child_depth > 0 ? nchild : 0;
+        if (W.child_sort)  // (kernel argument: block-uniform, every thread reaches the barriers)
+            at = block_append_keyed(W.lvl + L + 1, nc, nchild > 0 ? octant(ch0.dir) : 0, nchild > 1 ? octant(ch1.dir) : 0,
+                                    co[0], co[1]);
+        else
+            at = block_append<256>(W.lvl + L + 1, nc);
+    }
     // ---- stores ----
     if (prim == NO_RAY) {
         if (in) store_node(W, i, f3(0, 0, 0), 0u);
@@ -666,6 +671,8 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         }
         return;
     }
+    if (nchild > 0 && unit_child(ch0)) out.info |= INFO_UNIT0;
+    if (nchild > 1 && unit_child(ch1)) out.info |= INFO_UNIT1;
     store_node(W, i, out.surf, out.info);
     if (out.info & INFO_LIT) {
         if (CHAIN || !W.bucket) store_hand(W, q, out.h);
@@ -767,7 +774,7 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
             const int src = lane0 + (int)k;
             light_color = add(light_color, f3(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src)));
         }
-        if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
+        if (n > 0) ret = add(ret, scale(light_color, Lt.inv_n));  // times(1 / samples)
     }
     return ret;
 }
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
             const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
             F3 light_color = f3(0, 0, 0);
             for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k));
-            if (n > 0) ret = add(ret, scale(light_color, 1.0 / n));
+            if (n > 0) ret = add(ret, scale(light_color, Lt.inv_n));  // times(1 / samples)
         }
         W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
         return;
@@ -834,7 +841,7 @@ struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
     }
 };
 
-template <int PF, bool CHAIN>
+template <int PF, bool CHAIN, bool FO>
 __global__ __launch_bounds__(256) void k_extend_q(DScene S, WArgs W, int L, double minD) {
     uint32_t count = W.npaths, base = 0;
     if (!CHAIN) {
@@ -843,7 +850,7 @@ __global__ __launch_bounds__(256) void k_extend_q(DScene S, WArgs W, int L, doub
         base = R.base;
     }
     ExtendSrc src{W, base};
-    persistent_cast<PF, false>(S, W.qctr + L, count, minD, DINF, true, src);
+    persistent_cast<PF, false, FO>(S, W.qctr + L, count, minD, DINF, true, src);
 }
 
 struct ShadowSrc {  // the light samples' shadow rays written by k_shadow_prep
@@ -887,12 +894,12 @@ __global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
     }
 }
 
-template <int PF, bool CHAIN>
+template <int PF, bool CHAIN, bool FO>
 __global__ __launch_bounds__(256) void k_shadow_cast(DScene S, WArgs W, int L) {
     uint32_t count = W.npaths;
     if (!CHAIN) count = level_range(W, L).count;
     ShadowSrc src{W};
-    persistent_cast<PF, true>(S, W.qctr + 32 + L, count * (uint32_t)W.group, 0.0001, 1, false, src);
+    persistent_cast<PF, true, FO>(S, W.qctr + 32 + L, count * (uint32_t)W.group, 0.0001, 1, false, src);
 }
 
 // colorFromLights' sums of k_shadow from the stored sample colours (shadowed: +0)
@@ -1005,8 +1012,11 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         ubs.push_back(ub);
         const int child_depth = A.max_depth - L - 1;
         timed(KT_EXTEND, [&] {
-            if (Q)
-                hipLaunchKernelGGL((k_extend_q<PF, CHAIN>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN>, ub)),
+            if (Q && S.sdf_all_forms)  // every SDF root a recognised form: the march without the VM
+                hipLaunchKernelGGL((k_extend_q<PF, CHAIN, true>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN, true>, ub)),
+                                   dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
+            else if (Q)
+                hipLaunchKernelGGL((k_extend_q<PF, CHAIN, false>), dim3(persistent_grid((const void *)k_extend_q<PF, CHAIN, false>, ub)),
                                    dim3(256), 0, st, S, W, L, L == 0 ? 0.0 : 0.0001);
             else
                 hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
@@ -1020,8 +1030,12 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 const size_t ne = ub * (size_t)W.group;
                 if (Q && W.ns <= 64) {
                     hipLaunchKernelGGL((k_shadow_prep<PF, CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
-                    hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN>), dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN>, ne)),
-                                       dim3(256), 0, st, S, W, L);
+                    if (S.sdf_all_forms)
+                        hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN, true>),
+                                           dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN, true>, ne)), dim3(256), 0, st, S, W, L);
+                    else
+                        hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN, false>),
+                                           dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN, false>, ne)), dim3(256), 0, st, S, W, L);
                     hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
                 } else if (W.ns <= 64)
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);

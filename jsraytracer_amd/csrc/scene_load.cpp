@@ -922,6 +922,7 @@ struct Loader {
             } else fail("unsupported light kind");
             // colorFromLights order: the light's samples in turn; each area sample draws twice
             const int32_t ns = L.kind == JSRT_LIGHT_POINT ? 1 : (int32_t)L.samples;
+            d.inv_n = ns > 0 ? 1.0 / ns : 0.0;  // colorFromLights: light_color.times(1 / samples)
             if (ns < 0 || S.sample_light.size() + (size_t)ns > 4096) fail("too many light samples per shading point");
             for (int32_t k = 0; k < ns; ++k) {
                 S.sample_light.push_back((int32_t)S.lights.size());
@@ -993,6 +994,11 @@ struct Loader {
                 S.sdf_range[2 * n] = fr.first;
                 S.sdf_range[2 * n + 1] = fr.second;
             }
+        S.sdf_all_forms = S.sdfg.empty() ? 0 : 1;
+        for (const jsrt_rec_sdfgeom &G : S.sdfg) {
+            const int32_t pc = S.sdf_range[2 * (size_t)G.root];
+            if (pc < 0 || S.sdf_insn[pc].op != SOP_FORM) S.sdf_all_forms = 0;
+        }
     }
 };
 

@@ -33,6 +33,7 @@ struct HostScene {
     std::vector<int32_t> sample_light, sample_call;  // per light sample of a node
     int32_t light_draws = 0;
     std::vector<SdfInsn> sdf_insn;
+    int32_t sdf_all_forms = 0;         // every SDF geometry root's program is a recognised form
     std::vector<double> sdf_const;
     std::vector<int32_t> sdf_range;
     std::vector<int32_t> sdf_child;
