@@ -27,8 +27,9 @@ INCLUDE = os.path.join(HERE, "..", "include")
 PUBLIC = ["jsrt.h", "jsrt_scene.h", "jsrt_mesh.h", "jsrt_json.h"]
 # objects: (object stem, source, extra defines, dependencies); an object is rebuilt only when these change
 UNITS = [("render", "render.hip", [], HEADERS + ["jsrt.h", "jsrt_scene.h"])]
-UNITS += [(f"render_pf{pf}", "render_pf.hip", [f"-DJSRT_PF={pf}"], HEADERS + ["jsrt.h", "jsrt_scene.h"])
-          for pf in PROFILES.values()]
+# each profile in three parts (render_pf.hip JSRT_PART: chain kernels, tree kernels, single-cast entries)
+UNITS += [(f"render_pf{pf}_{part}", "render_pf.hip", [f"-DJSRT_PF={pf}", f"-DJSRT_PART={part}"],
+           HEADERS + ["jsrt.h", "jsrt_scene.h"]) for pf in PROFILES.values() for part in range(3)]
 UNITS += [("capi", "capi.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
           ("scene_load", "scene_load.cpp", [], HEADERS + ["jsrt.h", "jsrt_scene.h"]),
           ("mesh_build", "mesh_build.cpp", [], ["jsrt_mesh.h", "jsrt_scene.h", "obj_parse.h"]),
@@ -87,7 +88,7 @@ def _build_locked(force, verbose, variant, defines, profiles):
         _build_locked(False, verbose, None, (), None)  # the default objects a partial variant links against
     jobs, objs = [], []
     for stem, src, defs, deps in UNITS:
-        mine = variant is not None and (profiles is None or any(stem == f"render_pf{p}" for p in profiles))
+        mine = variant is not None and (profiles is None or any(stem.startswith(f"render_pf{p}_") for p in profiles))
         o = _obj(stem, tag if mine else "")
         objs.append(o)
         if force or mine or _newer(o, _deps(src, deps)):

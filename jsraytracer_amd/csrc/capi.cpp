@@ -112,7 +112,8 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
                  o_sh0 = A.add(H.shade0), o_shI = A.add(H.shadeI), o_mc = A.add(H.mc), o_mcc = A.add(H.mc_const), o_lights = A.add(H.lights),
                  o_sl = A.add(H.sample_light), o_sc = A.add(H.sample_call),
                  o_insn = A.add(H.sdf_insn), o_const = A.add(H.sdf_const), o_range = A.add(H.sdf_range),
-                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg), o_ltris = A.add(H.ltris), o_plit = A.add(H.prim_lit);
+                 o_schild = A.add(H.sdf_child), o_snodes = A.add(H.sdf_nodes), o_sdfg = A.add(H.sdfg), o_ltris = A.add(H.ltris), o_plit = A.add(H.prim_lit),
+                 o_gmask = A.add(H.grid_mask);
     const size_t total = A.host.size() + 256;
     HIP_TRY(hipMalloc(&sc->dmem, total));
     HIP_TRY(hipMemcpy(sc->dmem, A.host.data(), A.host.size(), hipMemcpyHostToDevice));
@@ -147,6 +148,14 @@ int jsrt_scene_create(const void *blob, size_t n, int32_t device, jsrt_scene **o
     D.bvh_stack = H.bvh.empty() ? 0 : H.bvh_max_depth + 2;
     D.ltris = (const DTri *)(b + o_ltris);
     D.prim_lit = (const int32_t *)(b + o_plit);
+    D.grid_mask = (const uint64_t *)(b + o_gmask);
+    for (int k = 0; k < 3; ++k) {
+        D.grid_lo[k] = H.grid_lo[k];
+        D.grid_inv[k] = H.grid_inv[k];
+        D.grid_dim[k] = H.grid_dim[k];
+    }
+    D.grid_cells = H.grid_cells;
+    D.grid_masked = H.roots.size() <= 64 ? 1 : 0;
     D.sdf_insn = (const SdfInsn *)(b + o_insn);
     D.sdf_const = (const double *)(b + o_const);
     D.sdf_range = (const int32_t *)(b + o_range);

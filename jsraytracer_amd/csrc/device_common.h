@@ -90,9 +90,12 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h, uint32_t v) {
 // pixkey = mix(mix(seed, pixel), sample), hoisted per sample
 __device__ __forceinline__ double keyed_uniform(uint32_t pixkey, uint32_t node, uint32_t call) {
     const uint32_t h = mix32(mix32(pixkey, node), call);
-    const uint64_t hi = mix32(h, 0xA5A5A5A5u) >> 5;
-    const uint64_t lo = mix32(h, 0x5A5A5A5Au) >> 6;
-    return (double)(hi * 67108864ull + lo) * (1.0 / 9007199254740992.0);
+    const uint32_t hi = mix32(h, 0xA5A5A5A5u) >> 5;  // 27 bits
+    const uint32_t lo = mix32(h, 0x5A5A5A5Au) >> 6;  // 26 bits
+    // (hi * 2^26 + lo) * 2^-53 with every step exact in f64 (hi * 2^-27 and lo * 2^-53 are exact, their sum
+    // has at most 53 significant bits): the same double as the reference generator's, without the u64
+    // multiply and the u64 -> f64 conversion sequence
+    return fma((double)hi, 1.0 / 134217728.0, (double)lo * (1.0 / 9007199254740992.0));
 }
 struct Rng {
     uint32_t key, node, calls;
@@ -140,6 +143,10 @@ JSRT_HD F3 xf_dir(const double *m, F3 d) {  // w = 0: the 4th term only adds a z
 JSRT_HD F3 ray_point(F3 o, F3 d, double t) {
     return f3(o.x + (float)((double)d.x * t), o.y + (float)((double)d.y * t), o.z + (float)((double)d.z * t));
 }
+// Math.sin and Math.cos of one argument: OCML's sincos runs the argument reduction and the polynomial
+// pair once; its two results are bit for bit those of its sin and cos (both select from the same
+// reduction and the same sin/cos polynomial pair, ocml.bc __ocml_{sin,cos,sincos}_f64)
+__device__ __forceinline__ void sin_cos(double x, double &s, double &c) { sincos(x, &s, &c); }
 // Vec.cartesianToSpherical (math.js:189-193)
 __device__ __forceinline__ void cart_to_sph(F3 n, float &u, float &v) {
     u = (float)(0.5 + atan2((double)n.z, (double)n.x) / (2 * JS_PI));
@@ -823,8 +830,12 @@ __device__ __forceinline__ bool root_needed(const RootBound &RB, F3 o, float ix,
 // when its ray segment (minD, min(best, maxD)) provably misses that box, and the wave skips the
 // object when no lane needs it.  Skipped objects could not have produced an accepted hit, so the
 // closest hit (first minimum in World.objects order) is unchanged bit for bit.
+//
+// mask (wave-uniform, shadow casts): bit i clear = root i (< 64) cannot produce an accepted hit on any lane's
+// segment (scene_load.cpp shadow_grid), so the loop skips it without loading its record.
 template <int PF, bool ANY>
-__device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp) {
+__device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double minD, double maxD, bool transp,
+                                          uint64_t mask = ~0ull) {
     Hit best{DINF, -1, 0};
     const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
     const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
@@ -832,6 +843,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     bool live = true;
     float flim = (float)maxD;  // (float)min(best, maxD): the cull's far limit, updated with best
     for (int i = 0; i < S.n_roots; ++i) {
+        if (i < 64 && !((mask >> i) & 1ull)) continue;
         const DRoot &R = S.rootrec[i];
         const bool need = live && root_needed(R.rb, o, ix, iy, iz, oabs, fminD, flim);
         if (!__any(need)) continue;
@@ -1091,8 +1103,10 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
         if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Vec.spherePick().to4(1)
             const double theta = 2.0 * JS_PI * rng.next();
             const double phi = acos(2.0 * rng.next() - 1.0);
-            const double sin_phi = sin(phi);
-            local = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
+            double sin_t, cos_t, sin_phi, cos_phi;
+            sin_cos(theta, sin_t, cos_t);
+            sin_cos(phi, sin_phi, cos_phi);
+            local = f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
         } else {  // Square / Circle.sampleSurface (geometry.js:295-300, 326-331)
             const double a = rng.next() - 0.5;
             const double b = rng.next() - 0.5;
@@ -1141,8 +1155,10 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
     if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
         const double theta = 2.0 * JS_PI * rng.next();
         const double phi = acos(2.0 * rng.next() - 1.0);
-        const double sin_phi = sin(phi);
-        const F3 sp3 = f3((float)(cos(theta) * sin_phi), or0((float)cos(phi)), or0((float)(sin(theta) * sin_phi)));
+        double sin_t, cos_t, sin_phi, cos_phi;
+        sin_cos(theta, sin_t, cos_t);
+        sin_cos(phi, sin_phi, cos_phi);
+        const F3 sp3 = f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;
@@ -1164,7 +1180,9 @@ __device__ __forceinline__ void camera_ray(const DCamera &C, double x, double y,
            (float)((((double)dir.x * T[8] + (double)dir.y * T[9]) + (double)dir.z * T[10]) + 0.0 * T[11]));
     if (C.kind == JSRT_CAMERA_DOF) {
         const double a = rng.next() * 2 * JS_PI, rr = sqrt(rng.next());  // Vec.circlePick (math.js:175-179)
-        const float cx = (float)(rr * cos(a)), cy = (float)(rr * sin(a));
+        double sa, ca;
+        sin_cos(a, sa, ca);
+        const float cx = (float)(rr * ca), cy = (float)(rr * sa);
         const float sx = (float)((double)cx * C.sensor), sy = or0((float)((double)cy * C.sensor));
         const F3 off = f3((float)((((double)sx * T[0] + (double)sy * T[1]) + 0.0 * T[2]) + 0.0 * T[3]),
                           (float)((((double)sx * T[4] + (double)sy * T[5]) + 0.0 * T[6]) + 0.0 * T[7]),

@@ -156,6 +156,13 @@ struct DScene {
     const int32_t *prim_lit; // per prim: 1 if its material takes light samples (not Solid / Transparent)
     int32_t sdf_all_forms;   // every SDF geometry root is a recognised program form (sdf_forms.h)
     int32_t pad_forms;
+    // Spatial buckets of the shadow hand-off (scene_load.cpp shadow_grid): hit points binned on a grid of
+    // grid_cells <= 63 cells over the bounded top-level objects (bucket grid_cells: outside the grid), and
+    // per bucket the top-level objects a shadow segment from that cell to any light can meet
+    // (grid_mask[b] bit i: root i; the outside bucket holds every root).  grid_masked: n_roots <= 64.
+    const uint64_t *grid_mask;   // grid_cells + 1 entries
+    float grid_lo[3], grid_inv[3];
+    int32_t grid_dim[3], grid_cells, grid_masked, pad_grid;
 };
 
 // Dynamic LDS of a casting kernel over a scene with BVHs: per lane a traversal stack of bvh_stack

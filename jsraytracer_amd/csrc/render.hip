@@ -221,7 +221,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree) bytes += 2 * need(rays, 4);                            // path parent
     bytes += need(nodes, 16) + need(4 * nodes, 16);                  // node + child
     if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
-    bytes += need(7 * hands, 16) + need(64, 4);                      // hand-off + level counts
+    bytes += need(HAND_PLANES * hands, 16) + need(64, 4);            // hand-off + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
     if (tree) bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);  // buckets
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
@@ -244,7 +244,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     w.node = carve<float4>(p, nodes);
     w.child = carve<float4>(p, 4 * nodes);
     if (tree) { w.slot = carve<float4>(p, 2 * nodes); w.root = carve<float>(p, 3 * paths); }
-    w.hand = carve<float4>(p, 7 * hands);
+    w.hand = carve<float4>(p, HAND_PLANES * hands);
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
@@ -268,7 +268,7 @@ void Wavefront::release() {
 Wavefront::~Wavefront() { release(); }
 
 size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
-    const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = 7 * 16;
+    const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = HAND_PLANES * 16;
     const bool persist = (S.profile & PF_SDF) && S.all_roots_prims;
     size_t group = 1;
     while ((int)group < ns && ns <= 64) group *= 2;
@@ -459,6 +459,9 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         // profiles/r03_s3_ab.txt: bunny +5.5 %; cornell -0.8 %, its keyed append costing k_shade 3 ms)
         const char *cs = getenv("JSRT_CHILD_SORT");
         W.child_sort = cs ? (cs[0] == '1') : ((S.profile & PF_BVH) != 0);
+        // hand-off buckets keyed by the hit point's grid cell (shadow-root masks), or by hit primitive
+        const char *bg = getenv("JSRT_BUCKET_GRID");
+        W.bucket_grid = (W.bucket && S.grid_cells > 0 && bg && bg[0] == '1') ? 1 : 0;
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
         if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
         auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths

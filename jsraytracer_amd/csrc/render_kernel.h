@@ -58,7 +58,7 @@ struct WArgs {
     // record planes (plane stride nstride / hstride): every access is one coalesced 16-B load per lane
     float4 *child;     // [(2 * j + part) * nstride + i]: part 0 {col.xyz, w.x}, part 1 {w.y, w.z, k (f64)}
     float4 *slot;      // tree: [j * nstride + i] the child's colour
-    float4 *hand;      // [k * hstride + h], k < 7: shadow hand-off of a lit node (h: path / level index)
+    float4 *hand;      // [k * hstride + h], k < 6: shadow hand-off of a lit node (h: path / level index, render_levels.h store_hand)
     float *root;       // tree: [3 * path] root colours
     uint32_t *lvl;     // tree: [L] ray count of level L; [LVL_FLAG] overflow flag
     // persistent casts (SDF scenes, render.hip k_extend_q / k_shadow_*): work counters per level
@@ -79,6 +79,7 @@ struct WArgs {
     int32_t chain;     // schedule
     int32_t bucket;    // tree schedule: 0, or 1 + shift: k_shadow reads lit nodes bucketed by hit primitive >> shift (bkt)
     int32_t child_sort; // tree schedule: k_shade appends a block's children grouped by direction octant
+    int32_t bucket_grid; // bucketed hand-off keyed by the hit point's grid cell (DScene::grid_*), not the primitive
     size_t pool, level_cap;
     size_t nstride, hstride;  // plane strides of child / slot and of hand
     size_t sstride;           // entries of sray / scol (0: persistent casts not used)

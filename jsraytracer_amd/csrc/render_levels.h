@@ -117,6 +117,16 @@ __device__ __forceinline__ uint32_t block_append_keyed(uint32_t *counter, int n,
 }
 __device__ __forceinline__ int octant(F3 d) { return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0); }
 
+// Grid cell of a hit point (DScene::grid_*), grid_cells when outside the grid (or not finite)
+__device__ __forceinline__ int grid_cell(const DScene &S, F3 p) {
+    const float fx = (p.x - S.grid_lo[0]) * S.grid_inv[0], fy = (p.y - S.grid_lo[1]) * S.grid_inv[1],
+                fz = (p.z - S.grid_lo[2]) * S.grid_inv[2];
+    if (!(fx >= 0.0f && fx < (float)S.grid_dim[0] && fy >= 0.0f && fy < (float)S.grid_dim[1] && fz >= 0.0f &&
+          fz < (float)S.grid_dim[2]))
+        return S.grid_cells;
+    return (int)fx + S.grid_dim[0] * ((int)fy + S.grid_dim[1] * (int)fz);
+}
+
 
 __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {  // tree schedule
     const uint32_t p = W.parent[i];
@@ -163,10 +173,11 @@ __device__ __forceinline__ LevelRange level_range(const WArgs &W, int L) {
 // node's RNG frame (its light-sample draws come first, materials.js:244-257).
 struct Handoff {
     F3 pos, N, R, refr, diff, spec;
-    double kr, smoothness;
-    int32_t mkind;
+    double kr;
+    int32_t mkind, mat;
     uint32_t addr, key;
     uint32_t node;  // the node's level index (bucketed hand-off: where k_shadow writes its colour)
+    uint32_t mask;  // shadow-root mask index (DScene::grid_mask) of the node's hit point
 };
 struct NodeOut {
     F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
@@ -416,7 +427,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         out.h.spec = sd.spec;
         out.h.kr = sd.kr;
         out.h.mkind = mkind;
-        out.h.smoothness = M.smoothness;
+        out.h.mat = P.material;
         rng.calls = (uint32_t)S.light_draws;
     }
     int n = 0;
@@ -474,16 +485,25 @@ __device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, 
     const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
     return add(c, scale(mul(mul(v, f3(a.x, a.y, a.z)), f3(a.w, b.x, b.y)), k));
 }
+// Hand-off record: planes of one float4 per lit node (plane stride hstride), 80 B, plus a sixth plane
+// only where kr != 1 (FresnelPhong / path tracing with a finite ratio):
+//   0 {P, addr}  1 {N, key}  2 {R, node}  3 {diff, mat << 8 | mask | HAND_KR}  4 {spec, hi(kr)}
+//   5 {refr, lo(kr)}
+// The material's kind and smoothness are read from its record (S.mat) by the sample.  With kr == 1
+// colorFromLightSample never reads refr (materials.js:349-354), and a Phong material never reads kr.
+constexpr uint32_t HAND_KR = 0x80000000u;  // plane 5 holds refr and lo(kr); kr != 1
+constexpr int HAND_PLANES = 6;
 __device__ __forceinline__ void store_hand(const WArgs &W, uint32_t h, const Handoff &o) {
     float4 *p = W.hand + h;
     const size_t hs = W.hstride;
-    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f((uint32_t)o.mkind));
-    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f((uint32_t)__double2loint(o.kr)));
-    p[2 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f((uint32_t)__double2hiint(o.kr)));
-    p[3 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f(o.addr));
-    p[4 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(o.key));
-    p[5 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2loint(o.smoothness)));
-    p[6 * hs] = make_float4(u2f((uint32_t)__double2hiint(o.smoothness)), u2f(o.node), 0.0f, 0.0f);
+    const bool kr_plane = o.mkind != JSRT_MAT_PHONG && o.kr != 1.0;
+    const uint32_t tag = ((uint32_t)o.mat << 8) | (o.mask & 0xFFu) | (kr_plane ? HAND_KR : 0u);
+    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f(o.addr));
+    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f(o.key));
+    p[2 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f(o.node));
+    p[3 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(tag));
+    p[4 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2hiint(o.kr)));
+    if (kr_plane) p[5 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f((uint32_t)__double2loint(o.kr)));
 }
 
 // per pixel, the renderer's f32 accumulation of one sample (renderers.js:93-97, 52-61)
@@ -544,7 +564,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         }
         i = R.base + (live ? t : 0u);
     }
-    int hp = -1;
+    int hp = -1, b = 0;  // b: the hit's bucket
     if (live && W.prim[i] != NO_RAY) {
         const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
         const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
@@ -552,6 +572,13 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         W.prim[i] = h.prim;
         W.ctx[i] = h.ctx;
         hp = h.prim;
+        // grid bucket: the cell of the hit point in f32 (within ~1e-6 of material_data.position, which
+        // scene_load.cpp shadow_grid's grown cells cover; k_shade reads the bucket back from brank)
+        if (!CHAIN && W.bucket && hp >= 0) {
+            const float tf = (float)h.t;
+            b = W.bucket_grid ? grid_cell(S, f3(fmaf(d.x, tf, o.x), fmaf(d.y, tf, o.y), fmaf(d.z, tf, o.z)))
+                              : hp >> (W.bucket - 1);
+        }
     }
     if (!CHAIN && W.bucket) {
         // Bucketed hand-off: ranks every lit hit (S.prim_lit: shade_node lights every hit but Solid /
@@ -561,7 +588,6 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         // waits for the block's slowest cast, and the atomics overlap other blocks' casts (as a
         // separate pass they cost cornell 30 ms per frame, r02_s16).
         const bool lit = hp >= 0 && S.prim_lit[hp] != 0;
-        const int b = lit ? hp >> (W.bucket - 1) : 0;
         const int lane = (int)__lane_id();
         const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
         uint64_t todo = __ballot(lit);
@@ -572,7 +598,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
             uint32_t base = 0;
             if (lane == first) base = atomicAdd(&hist[bv], (uint32_t)__popcll(m));
             base = __shfl(base, first);
-            if (lit && b == bv) W.brank[i] = base + (uint32_t)__popcll(m & lt);
+            if (lit && b == bv) W.brank[i] = ((uint32_t)bv << 16) | (base + (uint32_t)__popcll(m & lt));
             todo &= ~m;
         }
         __threadfence_block();
@@ -628,11 +654,14 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
         const Hit h{W.t[r], prim, W.ctx[r]};
         nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
         out.h.node = q;
+        out.h.mask = (uint32_t)S.grid_cells;  // every root
         if (!CHAIN && W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
-            const int b = prim >> (W.bucket - 1);
+            const uint32_t br = W.brank[r];      // bucket << 16 | rank in the block's bucket
+            const int b = (int)(br >> 16);
             const uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
-            hslot = B[2 * BKT_K + bucket_key(W, b)] + W.bbase[(size_t)blockIdx.x * BKT_N + b] + W.brank[r];
+            hslot = B[2 * BKT_K + bucket_key(W, b)] + W.bbase[(size_t)blockIdx.x * BKT_N + b] + (br & 0xFFFFu);
             if (hslot >= B[3 * BKT_K]) hslot = ~0u;  // (never: k_extend counted this node)
+            if (W.bucket_grid) out.h.mask = (uint32_t)b;
         }
     }
     // tree: children append to level L + 1; at depth 0 they are black without a cast
@@ -725,37 +754,45 @@ __global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene
 // delta, accepted distances (1e-4, 1), materials.js:250-252).
 template <int PF>
 __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
-    const float4 h0 = hp[0];
+    const float4 h0 = hp[0], h1 = hp[hs];
     P = f3(h0.x, h0.y, h0.z);
-    Rng rng{f2u(hp[4 * hs].w), f2u(hp[3 * hs].w), (uint32_t)S.sample_call[s]};
+    Rng rng{f2u(h1.w), f2u(h0.w), (uint32_t)S.sample_call[s]};
     F3 L, lcol;
     if (S.n_lights == 1)  // (kernel argument: uniform) the light record through scalar loads
         light_sample(S, as_const(S.lights)[0], P, rng, delta, L, lcol);
     else
         light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
-    const float4 h1 = hp[hs], h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs], h5 = hp[5 * hs], h6 = hp[6 * hs];
+    const float4 h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs];
+    const uint32_t tag = f2u(h3.w);
+    const jsrt_rec_material &M = S.mat[(tag & ~HAND_KR) >> 8];
     ShadeData sd;
     sd.N = f3(h1.x, h1.y, h1.z);
     sd.R = f3(h2.x, h2.y, h2.z);
-    sd.refr = f3(h3.x, h3.y, h3.z);
-    sd.diff = f3(h4.x, h4.y, h4.z);
-    sd.spec = f3(h5.x, h5.y, h5.z);
-    sd.kr = __hiloint2double((int)f2u(h2.w), (int)f2u(h1.w));
-    sd.smoothness = __hiloint2double((int)f2u(h6.x), (int)f2u(h5.w));
-    return light_sample_color((int)f2u(h0.w), sd, L, lcol);
+    sd.diff = f3(h3.x, h3.y, h3.z);
+    sd.spec = f3(h4.x, h4.y, h4.z);
+    sd.refr = f3(0, 0, 0);
+    sd.kr = 1.0;
+    if (tag & HAND_KR) {
+        const float4 h5 = hp[5 * hs];
+        sd.refr = f3(h5.x, h5.y, h5.z);
+        sd.kr = __hiloint2double((int)f2u(h4.w), (int)f2u(h5.w));
+    }
+    sd.smoothness = M.smoothness;
+    return light_sample_color((int)M.kind, sd, L, lcol);
 }
 
 __device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
 
 template <int PF>
-__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s) {
+__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s,
+                                           uint64_t mask = ~0ull) {
     F3 P, delta;
     const F3 c = sample_unshadowed<PF>(S, hp, hs, s, P, delta);
     // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
     if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return f3(0, 0, 0);
-    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false);
+    const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false, mask);
     if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
     return c;
 }
@@ -793,9 +830,22 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     const uint32_t s = e % G;
     bool in = q < count;
     const float4 *hp = W.hand + (in ? q : 0u);
+    uint32_t mi = 0;  // the node's shadow-root mask (grid cell of its hit point)
     if (!CHAIN && !SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
         in = q < as_const(W.bkt + (size_t)L * BKT_LEVEL)[3 * BKT_K];
-        q = in ? f2u(hp[6 * W.hstride].y) : 0u;
+        q = in ? f2u(hp[2 * W.hstride].w) : 0u;
+        mi = f2u(hp[3 * W.hstride].w) & 0xFFu;
+    }
+    // Shadow-root mask of the wave (scene_load.cpp shadow_grid): when every node of the wave has its hit
+    // point in one grid cell -- the hand-off is bucketed by cell, so nearly every wave -- the world loop
+    // visits only the roots a shadow segment from that cell can meet.
+    uint64_t mask = ~0ull;
+    if (!CHAIN && !SERIAL && W.bucket && W.bucket_grid && S.grid_masked) {
+        const uint64_t on = __ballot(in);
+        if (on) {
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mi, __builtin_ctzll(on));
+            if (!__ballot(in && mi != m0) && m0 <= (uint32_t)S.grid_cells) mask = as_const(S.grid_mask)[m0];
+        }
     }
     const uint32_t i = base + (in ? q : 0u);
     const float4 nd = W.node[i];
@@ -815,7 +865,7 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
         return;
     }
     F3 c = f3(0, 0, 0);
-    if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s);
+    if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s, mask);
     ret = light_sums(S, G, ret, c);
     if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }

@@ -6,13 +6,25 @@
 #error "compile with -DJSRT_PF=<kernel profile>"
 #endif
 
+// -DJSRT_PART=0|1|2 splits a profile into three objects compiled in parallel (build.py): the chain
+// schedule's kernels, the tree schedule's, and the single-cast entries (jsrt_cast / jsrt_material_data).
+#ifndef JSRT_PART
+#define JSRT_PART -1
+#endif
+
 namespace jsrt {
+#if JSRT_PART < 0 || JSRT_PART == 0
 template void run_batch<JSRT_PF, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t, KernelTimes *,
                                        const std::vector<size_t> &);
+#endif
+#if JSRT_PART < 0 || JSRT_PART == 1
 template void run_batch<JSRT_PF, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t, KernelTimes *,
                                         const std::vector<size_t> &);
+#endif
+#if JSRT_PART < 0 || JSRT_PART == 2
 template void cast_rays_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double, double, int, double *, int32_t *,
                                    hipStream_t);
 template void material_data_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double *, int32_t *, float *, float *,
                                         float *, float *, float *, hipStream_t);
+#endif
 }  // namespace jsrt

@@ -999,6 +999,107 @@ struct Loader {
             const int32_t pc = S.sdf_range[2 * (size_t)G.root];
             if (pc < 0 || S.sdf_insn[pc].op != SOP_FORM) S.sdf_all_forms = 0;
         }
+        shadow_grid();
+    }
+
+    // Spatial buckets of the shadow hand-off and their shadow-root masks (DScene::grid_*).
+    //
+    // The grid spans the bounded top-level objects' cull boxes with at most 63 cells (as cubic as the
+    // extents allow); a hit point outside it goes to bucket grid_cells.  A shadow ray of a lit node in
+    // cell c starts at the hit point P (in c, up to the rounding of the cell index, covered by growing
+    // the cell by 1e-4 of the grid) and ends at delta = Q - P, Q a light sample point (in the light's
+    // world box, grown for the f32 rounding of Q and of the subtraction): the segment lies in the box
+    // hull(cell, light boxes).  A root whose cull box (RootBound: lo/hi grown by k |P|_inf + e0, with
+    // the largest |P|_inf of the cell) misses that hull cannot produce an accepted shadow hit from any
+    // point of the cell -- world_cast's own cull (root_needed) would reject it on every such ray -- so
+    // the cell's mask leaves it out.  Unbounded roots are in every mask; the outside bucket's mask holds
+    // every root.
+    void shadow_grid() {
+        const size_t nr = S.roots.size();
+        const uint64_t all = nr >= 64 ? ~0ull : ((1ull << nr) - 1);
+        S.grid_cells = 0;
+        S.grid_mask.assign(1, all);
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool any = false;
+        for (const RootBound &rb : S.rbounds)
+            if (rb.bounded) {
+                any = true;
+                for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], rb.lo[k]); hi[k] = fmax(hi[k], rb.hi[k]); }
+            }
+        if (!any) return;
+        double ext[3];
+        for (int k = 0; k < 3; ++k) ext[k] = fmax(hi[k] - lo[k], 1e-6 * fmax(1.0, fmax(fabs(lo[k]), fabs(hi[k]))));
+        int dim[3] = {1, 1, 1};
+        double best = INFINITY;
+        const char *gm = getenv("JSRT_GRID_MAX");  // A/B: fewer, larger cells
+        const int cmax = gm ? std::max(1, std::min(63, atoi(gm))) : 63;
+        for (int x = 1; x <= cmax; ++x)
+            for (int y = 1; x * y <= cmax; ++y)
+                for (int z = 1; x * y * z <= cmax; ++z) {
+                    const double w = fmax(ext[0] / x, fmax(ext[1] / y, ext[2] / z));
+                    if (w < best * (1 - 1e-9) || (w <= best * (1 + 1e-9) && x * y * z > dim[0] * dim[1] * dim[2])) {
+                        best = w;
+                        dim[0] = x; dim[1] = y; dim[2] = z;
+                    }
+                }
+        // light sample points: a point light's position; an area light's surface through its transform
+        // (Square / Circle sample [-0.5, 0.5]^2 x {0}, a Sphere the unit sphere, lights.js:80-92)
+        double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (const DLight &L : S.lights) {
+            double c[3], h[3];
+            if (L.kind == JSRT_LIGHT_POINT) {
+                for (int k = 0; k < 3; ++k) { c[k] = L.pos[k]; h[k] = 0; }
+            } else {
+                const double lh[3] = {L.gkind == JSRT_GEOM_SPHERE ? 1.0 : 0.5, L.gkind == JSRT_GEOM_SPHERE ? 1.0 : 0.5,
+                                      L.gkind == JSRT_GEOM_SPHERE ? 1.0 : 0.0};
+                for (int k = 0; k < 3; ++k) {
+                    c[k] = L.T[4 * k + 3];
+                    h[k] = fabs(L.T[4 * k]) * lh[0] + fabs(L.T[4 * k + 1]) * lh[1] + fabs(L.T[4 * k + 2]) * lh[2];
+                }
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double g = 1e-5 * (fabs(c[k]) + h[k] + 1.0);
+                llo[k] = fmin(llo[k], c[k] - h[k] - g);
+                lhi[k] = fmax(lhi[k], c[k] + h[k] + g);
+            }
+        }
+        for (int k = 0; k < 3; ++k)
+            if (!isfinite(llo[k]) || !isfinite(lhi[k])) return;  // no lights, or one that is not bounded
+        const int cells = dim[0] * dim[1] * dim[2];
+        S.grid_mask.assign(cells + 1, all);
+        const double grow = 1e-4 * fmax(ext[0], fmax(ext[1], ext[2])) + 1e-6;
+        for (int c = 0; c < cells; ++c) {
+            const int ci[3] = {c % dim[0], (c / dim[0]) % dim[1], c / (dim[0] * dim[1])};
+            double a[3], b[3], oabs = 0;
+            for (int k = 0; k < 3; ++k) {
+                const double w = ext[k] / dim[k];
+                a[k] = lo[k] + ci[k] * w - grow;
+                b[k] = lo[k] + (ci[k] + 1) * w + grow;
+                oabs = fmax(oabs, fmax(fabs(a[k]), fabs(b[k])));
+            }
+            uint64_t m = 0;
+            for (size_t r = 0; r < nr && r < 64; ++r) {
+                const RootBound &rb = S.rbounds[r];
+                bool need = !rb.bounded;
+                if (!need) {
+                    need = true;
+                    for (int k = 0; k < 3 && need; ++k) {
+                        const double hlo = fmin(a[k], llo[k]), hhi = fmax(b[k], lhi[k]);
+                        const double g = 1e-5 * (fabs(hlo) + fabs(hhi) + 1.0);
+                        const double e = 1.01 * ((double)rb.k * oabs + (double)rb.e0) + 1e-5 * (fabs(rb.lo[k]) + fabs(rb.hi[k]) + 1.0);
+                        need = (double)rb.lo[k] - e <= hhi + g && (double)rb.hi[k] + e >= hlo - g;
+                    }
+                }
+                if (need) m |= 1ull << r;
+            }
+            S.grid_mask[c] = nr <= 64 ? m : all;
+        }
+        S.grid_cells = cells;
+        for (int k = 0; k < 3; ++k) {
+            S.grid_dim[k] = dim[k];
+            S.grid_lo[k] = (float)lo[k];
+            S.grid_inv[k] = (float)(dim[k] / ext[k]);
+        }
     }
 };
 

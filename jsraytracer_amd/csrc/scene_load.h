@@ -48,6 +48,10 @@ struct HostScene {
     // workload facts used for algorithmic-byte accounting
     int64_t n_bvh_nodes = 0, n_triangles = 0;
     int32_t bvh_max_depth = 0;  // deepest BVH node (root = 0): sizes the LDS traversal stack
+    // shadow hand-off grid (DScene::grid_*): cells, their root masks (+ the outside bucket's)
+    std::vector<uint64_t> grid_mask;
+    float grid_lo[3] = {0, 0, 0}, grid_inv[3] = {0, 0, 0};
+    int32_t grid_dim[3] = {0, 0, 0}, grid_cells = 0;
 };
 
 // Returns 0 on success; otherwise fills err.
