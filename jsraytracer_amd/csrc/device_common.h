@@ -26,16 +26,28 @@ namespace jsrt {
 // --------------------------------------------------------------------------------------------
 // JS scalar semantics
 JSRT_HD bool is_nan(double x) { return x != x; }
+// Math.max / Math.min as compares and selects (no branches): NaN if either operand is NaN (a NaN `a`
+// is returned as is, a NaN `b` is the select's fall-through); equal operands -- +-0 pairs included --
+// give the AND (max) / OR (min) of their bit patterns: +0 unless both are -0 for max, -0 if either is
+// for min, and the common value for equal non-zero operands (identical bits).
 JSRT_HD double js_max(double a, double b) {  // Math.max
-    if (is_nan(a) || is_nan(b)) return __builtin_nan("");
-    if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) && __builtin_signbit(b)) ? -0.0 : 0.0;
-    return a > b ? a : b;
+    double r = a > b ? a : b;
+    if (a == b) r = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, a) & __builtin_bit_cast(uint64_t, b));
+    return a != a ? a : r;
 }
 JSRT_HD double js_min(double a, double b) {  // Math.min
-    if (is_nan(a) || is_nan(b)) return __builtin_nan("");
-    if (a == 0.0 && b == 0.0) return (__builtin_signbit(a) || __builtin_signbit(b)) ? -0.0 : 0.0;
-    return a < b ? a : b;
+    double r = a < b ? a : b;
+    if (a == b) r = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, a) | __builtin_bit_cast(uint64_t, b));
+    return a != a ? a : r;
 }
+// the same on f32 values (exact: the result is an operand, +-0 or NaN)
+JSRT_HD float js_maxf(float a, float b) {
+    float r = a > b ? a : b;
+    if (a == b) r = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, a) & __builtin_bit_cast(uint32_t, b));
+    return a != a ? a : r;
+}
+JSRT_HD float js_max0f(float x) { return (x > 0.0f || x != x) ? x : 0.0f; }  // Math.max(x, 0)
+JSRT_HD float js_min0f(float x) { return x > 0.0f ? 0.0f : x; }              // Math.min(x, 0)
 JSRT_HD double js_sign(double x) {
     if (is_nan(x) || x == 0.0) return x;
     return x > 0 ? 1.0 : -1.0;
@@ -134,7 +146,8 @@ JSRT_HD F3 xf_point(const T *m, F3 o) {  // w = 1 (T: double in any address spac
               (float)((((double)o.x * m[4] + (double)o.y * m[5]) + (double)o.z * m[6]) + m[7]),
               (float)((((double)o.x * m[8] + (double)o.y * m[9]) + (double)o.z * m[10]) + m[11]));
 }
-JSRT_HD F3 xf_dir(const double *m, F3 d) {  // w = 0: the 4th term only adds a zero
+template <class T>
+JSRT_HD F3 xf_dir(const T *m, F3 d) {  // w = 0: the 4th term only adds a zero
     return f3((float)(((double)d.x * m[0] + (double)d.y * m[1]) + (double)d.z * m[2]),
               (float)(((double)d.x * m[4] + (double)d.y * m[5]) + (double)d.z * m[6]),
               (float)(((double)d.x * m[8] + (double)d.y * m[9]) + (double)d.z * m[10]));
@@ -240,7 +253,8 @@ __device__ __forceinline__ int box_enter_f32(float cx, float cy, float cz, float
     return -1;
 }
 
-JSRT_HD double aabb_intersect(const float *c, const float *h, F3 o, F3 d, double minD, double maxD) {  // geometry.js:173-179
+template <class T>
+JSRT_HD double aabb_intersect(const T *c, const T *h, F3 o, F3 d, double minD, double maxD) {  // geometry.js:173-179
     double tmin, tmax;
     if (aabb_slab(c[0], c[1], c[2], h[0], h[1], h[2], o, d, minD, maxD, tmin, tmax)) return (tmin >= minD) ? tmin : tmax;
     return -(double)__builtin_inf();
@@ -297,8 +311,9 @@ __device__ __forceinline__ double sdf_box(const T *k, F3 P) {
     const float qx = fabsf(P.x) - (float)k[0];
     const float qy = or0(fabsf(P.y) - (float)k[1]);
     const float qz = or0(fabsf(P.z) - (float)k[2]);
-    const F3 m = f3((float)js_max(qx, 0), (float)js_max(qy, 0), (float)js_max(qz, 0));
-    return sqrt(dot3(m, m)) + js_min(js_max(js_max(qx, qy), qz), 0);
+    // Math.max / Math.min of f32 values are f32 values: evaluated in f32 (js_maxf)
+    const F3 m = f3(js_max0f(qx), js_max0f(qy), js_max0f(qz));
+    return sqrt(dot3(m, m)) + (double)js_min0f(js_maxf(js_maxf(qx, qy), qz));
 }
 
 // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473): Math.fmod(p + s/2, s) - s/2 per axis.
@@ -633,8 +648,8 @@ struct Hit {
     int ctx;
 };
 
-template <int PF>
-__device__ __forceinline__ double prim_intersect_local(const DScene &S, const DPrim &P, F3 o, F3 d, double minD,
+template <int PF, class PT>  // PT: DPrim in any address space
+__device__ __forceinline__ double prim_intersect_local(const DScene &S, const PT &P, F3 o, F3 d, double minD,
                                                        double maxD) {
     switch (P.gkind) {
     case JSRT_GEOM_PLANE: return plane_t(o, d);
@@ -667,10 +682,12 @@ __device__ __forceinline__ double prim_intersect_local(const DScene &S, const DP
 }
 
 // one row of Mat x Vec (math.js:392-397), the same operations as xf_point / xf_dir
-JSRT_HD float xf_row_point(const double *r, F3 o) {
+template <class T>
+JSRT_HD float xf_row_point(const T *r, F3 o) {
     return (float)((((double)o.x * r[0] + (double)o.y * r[1]) + (double)o.z * r[2]) + r[3]);
 }
-JSRT_HD float xf_row_dir(const double *r, F3 d) {
+template <class T>
+JSRT_HD float xf_row_dir(const T *r, F3 d) {
     return (float)(((double)d.x * r[0] + (double)d.y * r[1]) + (double)d.z * r[2]);
 }
 
@@ -678,7 +695,8 @@ JSRT_HD float xf_row_dir(const double *r, F3 d) {
 // `inv` (rows 0..2), for a caller that accepts minD < t < lim: a planar primitive whose plane
 // distance already fails that test may return it without transforming the x/y rows or testing its
 // bounds; the caller's decision is unchanged.
-JSRT_HD double planar_intersect(int k, const double *inv, F3 o, F3 d, double minD, double lim) {
+template <class T>
+JSRT_HD double planar_intersect(int k, const T *inv, F3 o, F3 d, double minD, double lim) {
     // SimplePlane.intersect (geometry.js:246-248) needs only the local z row
     const float oz = xf_row_point(inv + 8, o), dz = xf_row_dir(inv + 8, d);
     const double t = (dz != 0.0f) ? -(double)oz / (double)dz : -(double)__builtin_inf();
@@ -695,8 +713,8 @@ JSRT_HD double planar_intersect(int k, const double *inv, F3 o, F3 d, double min
 // `lim` = the caller's acceptance bound min(best, maxD): every caller accepts a distance only when
 // minD < t < lim, so a planar primitive whose plane distance already fails that test may return it
 // without transforming the x/y rows or testing its bounds; the caller's decision is unchanged.
-template <int PF>
-__device__ __forceinline__ double prim_intersect(const DScene &S, const DPrim &P, F3 o, F3 d, double minD, double maxD,
+template <int PF, class PT>  // PT: DPrim in any address space
+__device__ __forceinline__ double prim_intersect(const DScene &S, const PT &P, F3 o, F3 d, double minD, double maxD,
                                                  bool transp, double lim) {
     if (!transp && !P.casts_shadow) return DINF;
     const int k = P.gkind;
@@ -805,7 +823,8 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
 // Conservative cull of one top-level object: false only when the object provably
 // cannot produce an accepted hit on the segment (minD, flim): the ray misses its world box inflated
 // by k|o| + e0 (flim = (float) of the far limit min(best, maxD)).
-__device__ __forceinline__ bool root_needed(const RootBound &RB, F3 o, float ix, float iy, float iz, float oabs,
+template <class RBT>  // RootBound in any address space
+__device__ __forceinline__ bool root_needed(const RBT &RB, F3 o, float ix, float iy, float iz, float oabs,
                                             float fminD, float flim) {
     if (!RB.bounded) return true;
     const float e = RB.k * oabs + RB.e0;
@@ -844,7 +863,9 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
     float flim = (float)maxD;  // (float)min(best, maxD): the cull's far limit, updated with best
     for (int i = 0; i < S.n_roots; ++i) {
         if (i < 64 && !((mask >> i) & 1ull)) continue;
-        const DRoot &R = S.rootrec[i];
+        // the record of a wave-uniform root through the constant address space: scalar loads into SGPRs
+        // (a generic pointer gets a vector load per field, each waited for on the loop's critical path)
+        const auto &R = as_const(S.rootrec)[i];
         const bool need = live && root_needed(R.rb, o, ix, iy, iz, oabs, fminD, flim);
         if (!__any(need)) continue;
         if (!need) {  // (a divergent if, not a divergent continue: the loop itself stays uniform)
@@ -859,7 +880,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
                 }
             }
         } else if ((PF & PF_BVH) && R.kind == INST_BVH) {
-            const double *m = R.p.inv;
+            const auto *m = R.p.inv;
             const Hit h = bvh_cast<PF, ANY>(S, S.insts[R.inst], xf_point(m, o), xf_dir(m, d), minD, maxD, transp);
             if (h.prim >= 0 && h.t > minD && h.t < best.t && h.t < maxD) {
                 best = h;

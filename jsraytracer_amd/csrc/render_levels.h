@@ -17,6 +17,9 @@
 #ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade (register budget)
 #define JSRT_SHADE_OCC 2
 #endif
+#ifndef JSRT_SHADE_OCC_FLAT  // analytic profile: 5 waves (95 VGPRs, 8 spilled) beat 4 (105): cornell +2.4 %, r03_s14
+#define JSRT_SHADE_OCC_FLAT 5
+#endif
 // k_shadow / k_extend: at least 6 / 5 waves per SIMD.  Their casts are latency-bound (BVH node and
 // scene loads on a dependent chain), so more resident waves beat the registers the compiler would
 // otherwise keep (A/B on MI355X: cornell +3 %, bunny +15 %, dragon +4 % against no bound; 8 waves
@@ -308,11 +311,24 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
     case JSRT_GEOM_SDF: {  // SDFGeometry.materialData (sdf.js:41-47)
         if (!(PF & PF_SDF)) break;
         const jsrt_rec_sdfgeom &G = S.sdfg[P.gindex];
-        const double dist0 = sdf_node_dist(S, G.root, pl);
+        // the distance at pl and at the three offset points (sdf.js:41-47), from one evaluation site in
+        // a loop: the form's straight-line code or the VM is emitted once, not four times (Menger k_shade
+        // 72 -> 64 ms, r03_s14)
         const float step = (float)G.normal_step;
-        const float nx = (float)((sdf_node_dist(S, G.root, f3(pl.x + step, pl.y + 0.0f, pl.z + 0.0f)) - dist0) / G.normal_step);
-        const float ny = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + step, pl.z + 0.0f)) - dist0) / G.normal_step);
-        const float nz = (float)((sdf_node_dist(S, G.root, f3(pl.x + 0.0f, pl.y + 0.0f, pl.z + step)) - dist0) / G.normal_step);
+        double dd[4] = {0, 0, 0, 0};
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            const F3 q = f3(pl.x + (k == 1 ? step : 0.0f), pl.y + (k == 2 ? step : 0.0f), pl.z + (k == 3 ? step : 0.0f));
+            const double r = S.sdf_all_forms ? sdf_form_dist(S, G.root, q) : sdf_node_dist(S, G.root, q);
+            dd[0] = k == 0 ? r : dd[0];
+            dd[1] = k == 1 ? r : dd[1];
+            dd[2] = k == 2 ? r : dd[2];
+            dd[3] = k == 3 ? r : dd[3];
+        }
+        const double dist0 = dd[0];
+        const float nx = (float)((dd[1] - dist0) / G.normal_step);
+        const float ny = (float)((dd[2] - dist0) / G.normal_step);
+        const float nz = (float)((dd[3] - dist0) / G.normal_step);
         const SdfMD md = sdf_material(S, G.root, pl);
         if (md.has_bc) { basecolor = md.bc; has_bc = 1; }
         if (md.has_uv) { u = md.u; v = md.v; has_uv = 1; }
@@ -620,7 +636,8 @@ __global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L);
 // Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
 // Tree schedule: node = pool slot; children are appended to level L + 1 (block-aggregated).
 template <int PF, bool CHAIN>
-__global__ __launch_bounds__(256, JSRT_SHADE_OCC) SHADE_ATTR void k_shade(DScene S, WArgs W, int L, int child_depth) {
+__global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
+    DScene S, WArgs W, int L, int child_depth) {
     const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
     uint32_t count = W.npaths, base = 0, next_base = 0;
     if (!CHAIN) {
