@@ -72,15 +72,20 @@ __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L) {
     const uint32_t tt = blockIdx.x * 256 + threadIdx.x;
     if (tt >= R.count) return;
     const uint32_t i = R.base + tt;
+    // the node record, its parent and its first child's colour and record are loaded together (most
+    // nodes have exactly one child): one memory round trip instead of two dependent ones
     const float4 nd = W.node[i];
-    const uint32_t p = W.parent[i];  // issued with the node record, not after the child loads
+    const uint32_t p = W.parent[i];
+    const float4 v0 = W.slot[i];
+    const float4 c0 = W.child[i];
     const uint32_t info = f2u(nd.w);
     if (!(info & INFO_HIT) || p == DEAD_RAY) return;
     F3 c = f3(nd.x, nd.y, nd.z);
     const int n = (int)((info >> INFO_NCHILD_SHIFT) & 3);
-    for (int j = 0; j < n; ++j) {
-        const float4 v = W.slot[(size_t)j * W.nstride + i];
-        c = add_child(W, i, (uint32_t)j, c, f3(v.x, v.y, v.z), info);
+    if (n > 0) c = add_child(W, i, 0u, c, f3(v0.x, v0.y, v0.z), info, &c0);
+    if (n > 1) {
+        const float4 v1 = W.slot[W.nstride + i];
+        c = add_child(W, i, 1u, c, f3(v1.x, v1.y, v1.z), info);
     }
     if (p == NO_PARENT) {  // write_result
         float *dst = W.root + 3 * (size_t)W.path[i];
@@ -459,9 +464,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         // profiles/r03_s3_ab.txt: bunny +5.5 %; cornell -0.8 %, its keyed append costing k_shade 3 ms)
         const char *cs = getenv("JSRT_CHILD_SORT");
         W.child_sort = cs ? (cs[0] == '1') : ((S.profile & PF_BVH) != 0);
-        // hand-off buckets keyed by the hit point's grid cell (shadow-root masks), or by hit primitive
+        // hand-off buckets keyed by the hit point's grid cell, with per-cell shadow-root masks, for flat
+        // scenes (cornell +1.5 %, r03_s15); by hit primitive (runs of consecutive triangles) for meshes,
+        // where the BVH and not the root loop carries the shadow casts (bunny +-0.2 %, r03_s6)
         const char *bg = getenv("JSRT_BUCKET_GRID");
-        W.bucket_grid = (W.bucket && S.grid_cells > 0 && bg && bg[0] == '1') ? 1 : 0;
+        const bool grid = bg ? bg[0] == '1' : S.profile == PF_ANALYTIC;
+        W.bucket_grid = (W.bucket && S.grid_cells > 0 && grid) ? 1 : 0;
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
         if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
         auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths

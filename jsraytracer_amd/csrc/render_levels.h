@@ -493,9 +493,10 @@ __device__ __forceinline__ void store_child(const WArgs &W, uint32_t i, uint32_t
 }
 // ((v * col) * w) * k added to c: surface.plus(child.times(col).times(w).times(k)) (materials.js:277-330).
 // info: the node's INFO_* word (INFO_UNIT0 / INFO_UNIT1: w = (1, 1, 1), k = 1, so the product is v * col).
-__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v, uint32_t info) {
+__device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, F3 c, F3 v, uint32_t info,
+                                       const float4 *first = nullptr) {  // first: the record's plane 0, if loaded
     const float4 *x = W.child + (size_t)(2 * j) * W.nstride + i;
-    const float4 a = x[0];
+    const float4 a = first ? *first : x[0];
     if (info & (j == 0 ? INFO_UNIT0 : INFO_UNIT1)) return add(c, mul(v, f3(a.x, a.y, a.z)));
     const float4 b = x[W.nstride];
     const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
