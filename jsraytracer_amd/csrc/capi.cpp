@@ -294,9 +294,9 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
             }
             return true;
         };
-    // default batch (A/B on MI355X, tools/ab_maxpaths.sh): 16 M paths for analytic scenes (cornell: 32 M
-    // loses 1 %), 32 M when the scene holds a BVH, triangles or an SDF (dragon +4 %, Menger +12 % over 16 M)
-    const size_t def_paths = (s->ds.profile & (PF_BVH | PF_TRI | PF_SDF)) ? (size_t)1 << 25 : (size_t)1 << 24;
+    // default batch (A/B on MI355X, tools/ab_maxpaths.sh): 32 M paths (dragon +4 %, Menger +12 % over
+    // 16 M; cornell, whose batches alternate between two pools and streams, +2.9 %: profiles/r03_s18_ab.txt)
+    const size_t def_paths = (size_t)1 << 25;
     size_t max_paths = (p && p->max_paths > 0) ? (size_t)p->max_paths : def_paths;
     if (const char *e = getenv("JSRT_MAX_PATHS")) max_paths = (size_t)atoll(e);
     // The batch's state is cached per scene and sized by max_paths (render_kernel.h

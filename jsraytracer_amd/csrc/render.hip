@@ -268,9 +268,14 @@ void Wavefront::release() {
     if (mem) (void)hipFree(mem);
     mem = nullptr;
     cap_bytes = 0;
+    if (twin) twin->release();
 }
 
-Wavefront::~Wavefront() { release(); }
+Wavefront::~Wavefront() {
+    release();
+    delete twin;
+    if (side) (void)hipStreamDestroy(side);
+}
 
 size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
     const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = HAND_PLANES * 16;
@@ -312,21 +317,21 @@ unsigned persistent_grid(const void *kernel, size_t work) {
 
 // instantiated in render_pf.hip, one translation unit per profile
 extern template void run_batch<PF_ANALYTIC, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_ANALYTIC, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_MESH, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_MESH, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_SDF, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_SDF, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_ALL, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 extern template void run_batch<PF_ALL, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t,
-                                         KernelTimes *, const std::vector<size_t> &);
+                                         KernelTimes *, const std::vector<size_t> &, const BatchSync *);
 
 #define JSRT_CAST_EXTERN(PFV) \
     extern template void cast_rays_pf<PFV>(const DScene &, const float *, uint32_t, double, double, int, double *, \
@@ -389,12 +394,12 @@ hipError_t cast_rays(const DScene &S, const float *d_rays, uint32_t n, double mi
 namespace {
 template <bool CHAIN>
 void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
-                  const std::vector<size_t> &bound) {
+                  const std::vector<size_t> &bound, const BatchSync *sync) {
     switch (S.profile) {
-    case PF_ANALYTIC: run_batch<PF_ANALYTIC, CHAIN>(S, A, W, st, kt, bound); break;
-    case PF_MESH: run_batch<PF_MESH, CHAIN>(S, A, W, st, kt, bound); break;
-    case PF_SDF: run_batch<PF_SDF, CHAIN>(S, A, W, st, kt, bound); break;
-    default: run_batch<PF_ALL, CHAIN>(S, A, W, st, kt, bound); break;
+    case PF_ANALYTIC: run_batch<PF_ANALYTIC, CHAIN>(S, A, W, st, kt, bound, sync); break;
+    case PF_MESH: run_batch<PF_MESH, CHAIN>(S, A, W, st, kt, bound, sync); break;
+    case PF_SDF: run_batch<PF_SDF, CHAIN>(S, A, W, st, kt, bound, sync); break;
+    default: run_batch<PF_ALL, CHAIN>(S, A, W, st, kt, bound, sync); break;
     }
 }
 }  // namespace
@@ -430,7 +435,37 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     }
     hipError_t e = hipSuccess;
     uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree schedule)
-    if (!chain && (e = hipHostMalloc((void **)&h_lvl, 64 * sizeof(uint32_t), 0)) != hipSuccess) return e;
+    if (!chain && (e = hipHostMalloc((void **)&h_lvl, 128 * sizeof(uint32_t), 0)) != hipSuccess) return e;
+    // Two batch pools on two streams: consecutive batches alternate between them, so one batch's levels
+    // (latency-bound casts, VALU-bound shadow samples, their launch tails) overlap the other's.  Only the
+    // accumulation into A.accum is ordered across them -- each batch's k_accum / k_resolve waits for the
+    // previous batch's (renderers.js:93-97: samples in order) -- so the image is unchanged bit for bit.
+    // (A/B on MI355X, profiles/r03_s18_ab.txt: cornell +12.5 %, the dragon +2.6 %, bunny +0.6 %; two
+    // persistent SDF marches side by side lose 1 %, so SDF scenes with persistent casts run on one
+    // stream.)  The twin pool is allocated only if it fits; otherwise the frame runs on one pool.
+    // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
+    const char *pe = getenv("JSRT_PERSIST");
+    const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
+    const uint64_t nbatches = (uint64_t)((A.spp + nsb - 1) / nsb) * ((npix_total + npix - 1) / npix);
+    const char *de = getenv("JSRT_DUAL");
+    bool dual = nbatches > 1 && (de ? de[0] == '1' : !persist);
+    hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_acc[2] = {nullptr, nullptr};
+    auto release_events = [&] {
+        for (hipEvent_t x : {ev_start, ev_end, ev_acc[0], ev_acc[1]})
+            if (x) (void)hipEventDestroy(x);
+    };
+    if (dual) {
+        if (!wf.twin) wf.twin = new Wavefront();
+        if (!wf.side) e = hipStreamCreateWithFlags(&wf.side, hipStreamNonBlocking);
+        for (hipEvent_t *x : {&ev_start, &ev_end, &ev_acc[0], &ev_acc[1]})
+            if (e == hipSuccess) e = hipEventCreateWithFlags(x, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            if (h_lvl) (void)hipHostFree(h_lvl);
+            release_events();
+            return e;
+        }
+    }
+    hipStream_t st2 = dual ? wf.side : st;
     bool conservative = false;
     double reported = 0;  // completion already reported: a redone frame reports only beyond it
     for (int attempt = 0; e == hipSuccess; ++attempt) {
@@ -439,15 +474,24 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         int group = 1;
         if (ns > 1 && ns <= 64)
             while (group < ns) group *= 2;
-        // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
-        const char *pe = getenv("JSRT_PERSIST");
-        const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
         // hand-off slots: one per node of a level; level 0 holds all `paths` camera rays, the
         // deeper levels at most level_cap (k_shade poisons the batch before writing past it)
         const size_t hands = chain ? paths : std::max(level_cap, paths);
         const size_t shadow = persist ? hands * (size_t)group : 0;
         e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
                   : wf.reserve(pool, pool, hands, paths, true, shadow);
+        if (e == hipSuccess && dual) {
+            const hipError_t e2 = chain ? wf.twin->reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
+                                        : wf.twin->reserve(pool, pool, hands, paths, true, shadow);
+            if (e2 == hipErrorOutOfMemory) {  // no room for a second pool: one pool, one stream
+                (void)hipGetLastError();
+                wf.twin->release();
+                dual = false;
+                st2 = st;
+            } else {
+                e = e2;
+            }
+        }
         if (e != hipSuccess) break;
         WArgs W = wf.args;
         W.ns = ns;
@@ -470,8 +514,35 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         const char *bg = getenv("JSRT_BUCKET_GRID");
         const bool grid = bg ? bg[0] == '1' : S.profile == PF_ANALYTIC;
         W.bucket_grid = (W.bucket && S.grid_cells > 0 && grid) ? 1 : 0;
+        WArgs W2 = W;  // the twin pool: the same settings over its own buffers
+        if (dual) {
+            const WArgs &t = wf.twin->args;
+            W2.ox = t.ox; W2.oy = t.oy; W2.oz = t.oz; W2.dx = t.dx; W2.dy = t.dy; W2.dz = t.dz;
+            W2.addr = t.addr; W2.key = t.key; W2.path = t.path; W2.parent = t.parent; W2.t = t.t;
+            W2.prim = t.prim; W2.ctx = t.ctx; W2.node = t.node; W2.child = t.child; W2.slot = t.slot;
+            W2.hand = t.hand; W2.root = t.root; W2.lvl = t.lvl; W2.qctr = t.qctr; W2.sray = t.sray;
+            W2.scol = t.scol; W2.bkt = t.bkt; W2.bbase = t.bbase; W2.brank = t.brank;
+        }
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
         if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
+        if (dual) {  // the side stream starts after everything enqueued on st so far
+            if ((e = hipEventRecord(ev_start, st)) != hipSuccess || (e = hipStreamWaitEvent(st2, ev_start, 0)) != hipSuccess) break;
+            if (!chain && (e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;
+        }
+        // the frame flags (and, for progress, level counts) of both pools, read back after both streams idle
+        auto read_flags = [&]() -> hipError_t {
+            hipError_t r;
+            if (dual && ((r = hipEventRecord(ev_end, st2)) != hipSuccess || (r = hipStreamWaitEvent(st, ev_end, 0)) != hipSuccess))
+                return r;
+            if (!chain) {
+                if ((r = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
+                if (dual && (r = hipMemcpyAsync(h_lvl + 64, W2.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+                    return r;
+            }
+            return hipStreamSynchronize(st);
+        };
+        auto flagged = [&](int k) { return h_lvl[k] != 0 || (dual && h_lvl[64 + k] != 0); };
+        uint64_t bi = 0;  // batch index: even batches on (W, st), odd ones on (W2, st2)
         auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths
             std::vector<size_t> b(depth, 0);
             size_t ub = np;
@@ -488,23 +559,30 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         bool stop = false;
         for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess && !stop; s0 += nsb) {
             const uint32_t nb = std::min<uint32_t>(nsb, (uint32_t)A.spp - s0);
-            for (uint32_t p0 = 0; p0 < npix_total; p0 += npix) {
-                W.p0 = p0;
-                W.npix = std::min(npix, npix_total - p0);
-                W.s0 = s0;
-                W.npaths = W.npix * nb;
-                const std::vector<size_t> bound = chain ? std::vector<size_t>() : bounds(W.npaths);
-                if (chain) run_batch_pf<true>(S, A, W, st, kt, bound);
-                else run_batch_pf<false>(S, A, W, st, kt, bound);
+            for (uint32_t p0 = 0; p0 < npix_total; p0 += npix, ++bi) {
+                const bool odd = dual && (bi & 1);
+                WArgs &Wb = odd ? W2 : W;
+                const hipStream_t sb = odd ? st2 : st;
+                Wb.p0 = p0;
+                Wb.npix = std::min(npix, npix_total - p0);
+                Wb.s0 = s0;
+                Wb.npaths = Wb.npix * nb;
+                const std::vector<size_t> bound = chain ? std::vector<size_t>() : bounds(Wb.npaths);
+                BatchSync sync;
+                if (dual) {
+                    sync.wait = bi > 0 ? ev_acc[(bi - 1) & 1] : nullptr;
+                    sync.done = ev_acc[bi & 1];
+                }
+                if (chain) run_batch_pf<true>(S, A, Wb, sb, kt, bound, &sync);
+                else run_batch_pf<false>(S, A, Wb, sb, kt, bound, &sync);
                 if ((e = hipGetLastError()) != hipSuccess) break;
-                done += (uint64_t)W.npix * nb;
+                done += (uint64_t)Wb.npix * nb;
                 if (kt) ++kt->batches;
                 if (progress && A.kind != JSRT_RENDERER_INCREMENTAL) {
                     // Simple / RandomMultisampling report {pass: 0, completion: pixels done / total} from
                     // inside their pixel loop (renderers.js:28-37): here after every batch
-                    if (!chain && (e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
-                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                    const bool clean = chain || (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]);
+                    if ((e = read_flags()) != hipSuccess) break;
+                    const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                     const double c = (double)done / (double)total;
                     if (c > reported) {
                         reported = c;
@@ -515,19 +593,18 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     // learn the level counts: from the scene's first batch, or -- when that batch was
                     // not representative and a frame had to be redone -- as the maximum over every
                     // batch of the conservative redo, so later frames of this shape are not redone
-                    if ((e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
-                    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+                    if ((e = hipMemcpyAsync(h_lvl, Wb.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, sb)) != hipSuccess) break;
+                    if ((e = hipStreamSynchronize(sb)) != hipSuccess) break;
                     if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) {
                         if (wf.frac.size() < (size_t)A.max_depth) wf.frac.assign(A.max_depth, 0.0);
                         for (int L = 0; L < A.max_depth; ++L)
-                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[L] / (double)W.npaths);
+                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[L] / (double)Wb.npaths);
                     }
                 }
             }
             if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL) {  // completion of finished work: wait for the pass
-                if (!chain && (e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
-                if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-                const bool clean = chain || (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]);
+                if ((e = read_flags()) != hipSuccess) break;
+                const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                 const double c = (double)done / (double)total;
                 if (c > reported) {
                     reported = c;
@@ -535,11 +612,13 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 }
             }
         }
+        if (e == hipSuccess && dual && chain) {  // st waits for the side stream's batches
+            if ((e = hipEventRecord(ev_end, st2)) == hipSuccess) e = hipStreamWaitEvent(st, ev_end, 0);
+        }
         if (e != hipSuccess || chain) break;
-        if ((e = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) break;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
-        if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) break;
-        if (h_lvl[LVL_FLAG]) {  // a batch outgrew the pool: twice the pool, relearn the counts
+        if ((e = read_flags()) != hipSuccess) break;
+        if (!flagged(LVL_FLAG) && !flagged(LVL_UNDER)) break;
+        if (flagged(LVL_FLAG)) {  // a batch outgrew the pool: twice the pool, relearn the counts
             if (paths * wf.pool_factor > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
             wf.pool_factor *= 2;
             wf.frac.clear();
@@ -549,7 +628,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         }
         if (kt) kt->reset();
     }
+    if (e != hipSuccess && dual) {  // nothing of this frame may still run on the side stream
+        (void)hipStreamSynchronize(st2);
+        (void)hipStreamSynchronize(st);
+    }
     if (h_lvl) (void)hipHostFree(h_lvl);
+    release_events();
     if (e != hipSuccess) return e;
     const bool ev = kt && kt->on(KT_FINAL);
     if (ev) kt->ev[KT_FINAL].begin(st);

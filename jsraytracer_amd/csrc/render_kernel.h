@@ -85,8 +85,18 @@ struct WArgs {
     size_t sstride;           // entries of sray / scol (0: persistent casts not used)
 };
 
+// Accumulation order across the two batch streams (render_frame): the batch's k_accum / k_resolve waits
+// for `wait` (the previous batch's accumulation, on the other stream) and records `done` after itself.
+struct BatchSync {
+    hipEvent_t wait = nullptr, done = nullptr;
+};
+
 struct Wavefront {  // owns the batch buffers (cached per scene)
     void *mem = nullptr;
+    // The second batch pool and the stream it runs on: consecutive batches alternate between two pools
+    // and two streams so one batch's levels overlap the other's (render_frame); created on first use.
+    Wavefront *twin = nullptr;
+    hipStream_t side = nullptr;
     // tree schedule, learned per scene and batch shape: pool size (x paths) and level counts
     size_t pool_paths = 0, pool_factor = 8;
     std::vector<double> frac;  // level L ray count / paths of the first batch

@@ -1060,7 +1060,9 @@ void material_data_pf(const DScene &S, const float *rays, uint32_t n, double *t,
 // levels are reduced bottom-up afterwards.
 template <int PF, bool CHAIN>
 void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t st, KernelTimes *kt,
-               const std::vector<size_t> &bound) {
+               const std::vector<size_t> &bound, const BatchSync *sync) {
+    auto accum_wait = [&] { if (sync && sync->wait) (void)hipStreamWaitEvent(st, sync->wait, 0); };
+    auto accum_done = [&] { if (sync && sync->done) (void)hipEventRecord(sync->done, st); };
     auto timed = [&](int which, auto launch) {
         const bool ev = kt && kt->on(which);
         if (ev) kt->ev[which].begin(st);
@@ -1112,12 +1114,16 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
             });
     }
     if (CHAIN) {
+        accum_wait();
         timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
+        accum_done();
         return;
     }
     for (int L = (int)ubs.size() - 1; L >= 0; --L)
         timed(KT_REDUCE, [&] { hipLaunchKernelGGL(k_reduce, dim3(grid_ub(ubs[L])), dim3(256), 0, st, W, L); });
+    accum_wait();
     timed(KT_ACCUM, [&] { hipLaunchKernelGGL(k_accum, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
+    accum_done();
 }
 
 }  // namespace jsrt

@@ -15,11 +15,11 @@
 namespace jsrt {
 #if JSRT_PART < 0 || JSRT_PART == 0
 template void run_batch<JSRT_PF, true>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t, KernelTimes *,
-                                       const std::vector<size_t> &);
+                                       const std::vector<size_t> &, const BatchSync *);
 #endif
 #if JSRT_PART < 0 || JSRT_PART == 1
 template void run_batch<JSRT_PF, false>(const DScene &, const RenderArgs &, const WArgs &, hipStream_t, KernelTimes *,
-                                        const std::vector<size_t> &);
+                                        const std::vector<size_t> &, const BatchSync *);
 #endif
 #if JSRT_PART < 0 || JSRT_PART == 2
 template void cast_rays_pf<JSRT_PF>(const DScene &, const float *, uint32_t, double, double, int, double *, int32_t *,
