@@ -188,7 +188,10 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
     its launches in the timed region (on the render stream)."""
     per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
     r = {"bound": bound, "kernel": dom, "avg_launch_ms": avg_ms, "launches_per_step": launches,
-         "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+         "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+         "timing_note": "avg_launch_ms is the HIP-event wall time of a launch on its stream; consecutive batches "
+                        "run on two streams (DESIGN.md §4.2), so other launches share the CUs during it and "
+                        "achieved / frac are per-launch rates under that overlap"}
     sec = avg_ms * 1e-3
     if per_sample:
         units_per_launch = per_sample * samples_per_frame / launches

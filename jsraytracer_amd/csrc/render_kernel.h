@@ -87,8 +87,13 @@ struct WArgs {
 
 // Accumulation order across the two batch streams (render_frame): the batch's k_accum / k_resolve waits
 // for `wait` (the previous batch's accumulation, on the other stream) and records `done` after itself.
+// aux (optional): the stream k_shadow runs on, so that level L's shadow samples overlap level L + 1's
+// closest-hit casts (they share no buffer); shade_done / shadow_done order k_shadow(L) after k_shade(L)
+// and k_shade(L + 1) -- which rewrites the hand-off -- after k_shadow(L).
 struct BatchSync {
     hipEvent_t wait = nullptr, done = nullptr;
+    hipStream_t aux = nullptr;
+    hipEvent_t shade_done = nullptr, shadow_done = nullptr;
 };
 
 struct Wavefront {  // owns the batch buffers (cached per scene)
@@ -97,6 +102,9 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     // and two streams so one batch's levels overlap the other's (render_frame); created on first use.
     Wavefront *twin = nullptr;
     hipStream_t side = nullptr;
+    // this pool's k_shadow stream and its two ordering events (BatchSync::aux), created on first use
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_shade = nullptr, ev_shadow = nullptr;
     // tree schedule, learned per scene and batch shape: pool size (x paths) and level counts
     size_t pool_paths = 0, pool_factor = 8;
     std::vector<double> frac;  // level L ray count / paths of the first batch

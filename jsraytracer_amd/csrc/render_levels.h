@@ -1063,11 +1063,14 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                const std::vector<size_t> &bound, const BatchSync *sync) {
     auto accum_wait = [&] { if (sync && sync->wait) (void)hipStreamWaitEvent(st, sync->wait, 0); };
     auto accum_done = [&] { if (sync && sync->done) (void)hipEventRecord(sync->done, st); };
+    const hipStream_t ss = (sync && sync->aux) ? sync->aux : st;  // k_shadow's stream
+    const bool split = ss != st;
     auto timed = [&](int which, auto launch) {
         const bool ev = kt && kt->on(which);
-        if (ev) kt->ev[which].begin(st);
+        const hipStream_t s = which == KT_SHADOW ? ss : st;
+        if (ev) kt->ev[which].begin(s);
         launch();
-        if (ev) kt->ev[which].end(st);
+        if (ev) kt->ev[which].end(s);
     };
     // dynamic LDS of the casting kernels: the BVH traversal stack (bvh_cast), 256 lanes x entries
     const size_t lds = (PF & (PF_BVH | PF_AGG)) ? bvh_lds_bytes(S, 256) : 0;
@@ -1092,11 +1095,17 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
         if (!CHAIN && W.bucket) hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(256), 0, st, W, L);
+        if (split && L > 0 && W.ns > 0) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the hand-off is free
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
         });
+        if (W.ns > 0 && split) {
+            (void)hipEventRecord(sync->shade_done, st);
+            (void)hipStreamWaitEvent(ss, sync->shade_done, 0);
+        }
         if (W.ns > 0)
             timed(KT_SHADOW, [&] {
+                const hipStream_t st = ss;  // (the launches below name `st`)
                 const size_t ne = ub * (size_t)W.group;
                 if (Q && W.ns <= 64) {
                     hipLaunchKernelGGL((k_shadow_prep<PF, CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
@@ -1112,7 +1121,9 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 else
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
             });
+        if (W.ns > 0 && split) (void)hipEventRecord(sync->shadow_done, ss);
     }
+    if (split && W.ns > 0 && !ubs.empty()) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the lit colours
     if (CHAIN) {
         accum_wait();
         timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
