@@ -189,9 +189,10 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
     per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
     r = {"bound": bound, "kernel": dom, "avg_launch_ms": avg_ms, "launches_per_step": launches,
          "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-         "timing_note": "avg_launch_ms is the HIP-event wall time of a launch on its stream; consecutive batches "
-                        "run on two streams (DESIGN.md §4.2), so other launches share the CUs during it and "
-                        "achieved / frac are per-launch rates under that overlap"}
+         "timing_note": "avg_launch_ms: HIP events around the kernel's launches in one instrumented step after the "
+                        "timed region; a render with per-launch events runs on one stream (its launches do not "
+                        "overlap other batches', DESIGN.md §4.2), so this is the kernel's own launch time -- the "
+                        "timed steps run the two-stream schedule without events"}
     sec = avg_ms * 1e-3
     if per_sample:
         units_per_launch = per_sample * samples_per_frame / launches
@@ -254,7 +255,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the frame's columns")
     ap.add_argument("--col-block", type=int, default=16)
-    ap.add_argument("--no-events", action="store_true", help="A/B: time steps without per-launch HIP events")
+    ap.add_argument("--events", action="store_true",
+                    help="bracket the dominant kernel's launches in the timed steps with HIP events (serialises the "
+                         "render onto one stream); by default the timed steps run the two-stream schedule without "
+                         "events and one instrumented one-stream step follows them")
     ap.add_argument("--spp", type=int, default=0, help="profiling only: override the config's spp (same launch "
                     "shapes, fewer batches); a bench line with it is not the config's number")
     args = ap.parse_args()
@@ -302,6 +306,7 @@ def main():
     tile = torch.zeros_like(fg.local, device=f"cuda:{local}") if host_tiles else fg.local
     stream = torch.cuda.current_stream().cuda_stream
     STAGES = jr._native.STAGES
+    ONE = jr._native.EVENTS_ONE_STREAM  # instrumented steps: every stage's own launch times (one stream)
 
     def step(events=None, colors=None):
         """events: None = no HIP events; 0 = every stage; else a bitmask of stages (jsrt.h stage_events)."""
@@ -317,7 +322,7 @@ def main():
     # warmup; the last warmup step is fully instrumented and names the dominant kernel
     st_full = None
     for w in range(max(args.warmup, 1)):
-        st_full = step(0 if w == max(args.warmup, 1) - 1 else None)
+        st_full = step(ONE if w == max(args.warmup, 1) - 1 else None)
     dom = max(st_full["stage_ms"], key=lambda k: st_full["stage_ms"][k])
     # timed region: HIP events bracket only the dominant kernel's launches (its average launch
     # duration for the roofline); events on every launch would add launch gaps to the step.  The last
@@ -328,7 +333,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step(None if args.no_events else (1 << STAGES.index(dom)), colors if k == args.steps - 1 else None)
+    stats = [step(((1 << STAGES.index(dom)) | ONE) if args.events else None, colors if k == args.steps - 1 else None)
              for k in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
@@ -340,12 +345,12 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
-    if args.no_events:
-        stats = [step(1 << STAGES.index(dom))]
+    if not args.events:  # the dominant kernel's launches, timed on the one-stream schedule
+        stats = [step((1 << STAGES.index(dom)) | ONE)]
     dom_ms = sum(s["stage_ms"][dom] for s in stats) / len(stats)
     dom_launches = stats[0]["stage_launches"][dom]
     # per-stage split: one more step after the timed region with every launch bracketed
-    st_after = step(0)
+    st_after = step(ONE)
     stage_ms, stage_launches, kernel_ms = st_after["stage_ms"], st_after["stage_launches"], st_after["kernel_ms"]
     torch.cuda.synchronize()
 
@@ -389,7 +394,8 @@ def main():
             "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
             "events_lost": {"timed": sum(x["events_lost"] for x in stats), "stage_split": st_after["events_lost"]},
             "frame_attempts": [x["attempts"] for x in stats],
-            "stages_note": "stage split from one fully-instrumented step after the timed region",
+            "stages_note": "stage split from one fully-instrumented step after the timed region, run on one "
+                           "stream so each launch's time is its own (the timed steps overlap two batch streams)",
             "stages_ms_per_step": {k: round(v, 3) for k, v in stage_ms.items() if v},
             "stage_launches_per_step": {k: v for k, v in stage_launches.items() if v},
             "counts_per_sample": {k: round(v, 4) for k, v in counts.items() if k != "samples"} if counts else None,

@@ -49,10 +49,14 @@ typedef struct {
     double timelimit_ms;     /* progress callback cadence (renderers.js:28-37); 0 = no callback */
     int32_t max_paths;       /* wavefront batch size in paths (<= 0: library default) */
     int32_t stage_events;    /* with stats: bitmask of the stages whose launches are bracketed by HIP
-                                events (bit k -> stage_ms[k]); 0 = all.  Events cost launch gaps. */
+                                events (bit k -> stage_ms[k]); 0 = all.  Events cost launch gaps.
+                                | JSRT_EVENTS_ONE_STREAM: run the render on one stream, so that a launch's
+                                event interval is its own time (consecutive batches otherwise overlap on
+                                two streams). */
     int32_t reserved[4];
 } jsrt_params;
 
+#define JSRT_EVENTS_ONE_STREAM ((int32_t)0x40000000)
 #define JSRT_STAGES 12
 typedef struct {
     double kernel_ms;        /* sum of all render-kernel durations (HIP events on the render stream) */

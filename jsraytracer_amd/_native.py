@@ -10,6 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JSRT_LIB") or os.path.join(HERE, "_build", "libjsrt.so")  # JSRT_LIB: A/B builds
 ABI_VERSION = 2  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
+EVENTS_ONE_STREAM = 0x40000000  # include/jsrt.h JSRT_EVENTS_ONE_STREAM (a Params.stage_events flag)
 
 
 class JsrtError(RuntimeError):

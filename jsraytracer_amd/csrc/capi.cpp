@@ -263,7 +263,8 @@ int run_launches(jsrt_scene *s, const jsrt_params *p, RenderArgs a, uint32_t *d_
         wf = own.get();
     }
     KernelTimes kt;
-    if (p && p->stage_events) kt.mask = (uint32_t)p->stage_events;
+    if (p && (p->stage_events & ~JSRT_EVENTS_ONE_STREAM)) kt.mask = (uint32_t)(p->stage_events & ~JSRT_EVENTS_ONE_STREAM);
+    kt.one_stream = p && (p->stage_events & JSRT_EVENTS_ONE_STREAM) != 0;
     auto t_last = std::chrono::steady_clock::now();
     const double tl = p ? p->timelimit_ms : 0;
     a.samples_per_batch = (p && p->samples_per_launch > 0) ? p->samples_per_launch : 0;

@@ -450,8 +450,14 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     const char *pe = getenv("JSRT_PERSIST");
     const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
     const uint64_t nbatches = (uint64_t)((A.spp + nsb - 1) / nsb) * ((npix_total + npix - 1) / npix);
+    // A render that asks for its launches' own times (JSRT_EVENTS_ONE_STREAM) runs on one stream: a
+    // launch's event interval is only its own time when no other batch's kernels share the CUs.
+    const bool timed_launches = kt && kt->one_stream;
     const char *de = getenv("JSRT_DUAL");
-    bool dual = nbatches > 1 && (de ? de[0] == '1' : !persist);
+    // two streams need two full batches: a frame of one full batch and a small remainder (bunny: 32 M + 1.2 M
+    // paths) has nothing to overlap
+    const bool two_full = (uint64_t)npix_total * (uint64_t)A.spp >= 2 * (uint64_t)npix * nsb;
+    bool dual = !timed_launches && nbatches > 1 && (de ? de[0] == '1' : (!persist && two_full));
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_acc[2] = {nullptr, nullptr};
     auto release_events = [&] {
         for (hipEvent_t x : {ev_start, ev_end, ev_acc[0], ev_acc[1]})
@@ -469,12 +475,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         }
     }
     hipStream_t st2 = dual ? wf.side : st;
-    // A frame on one stream (persistent SDF casts, one batch) runs k_shadow on a stream of its own
-    // (BatchSync::aux): level L's shadow samples overlap level L + 1's casts.  SDF_Menger +6.5 %; where
-    // two batch streams already overlap, it adds nothing (cornell +-0, bunny -0.8 %, dragon -1.3 %,
-    // profiles/r03_s18_ab.txt s22).  JSRT_SPLIT=0/1 forces it.
+    // A frame with persistent SDF casts (one stream) runs k_shadow on a stream of its own (BatchSync::aux):
+    // level L's shadow samples overlap level L + 1's march.  SDF_Menger +6.5 %; elsewhere it loses
+    // (bunny on one stream -5 %; beside two batch streams cornell +-0, dragon -1.3 %; profiles/
+    // r03_s18_ab.txt s22, s26).  JSRT_SPLIT=0/1 forces it.
     const char *se = getenv("JSRT_SPLIT");
-    const bool split = ns > 0 && (se ? se[0] == '1' : !dual);
+    const bool split = !timed_launches && ns > 0 && (se ? se[0] == '1' : (persist && !dual));
     auto aux_of = [&](Wavefront &w) -> hipError_t {
         hipError_t r = hipSuccess;
         if (!w.aux) r = hipStreamCreateWithFlags(&w.aux, hipStreamNonBlocking);

@@ -132,6 +132,7 @@ struct EventPairs {  // reusable HIP events bracketing every launch of one kerne
 struct KernelTimes {
     EventPairs ev[KT_N];
     uint32_t mask = ~0u;  // stages whose launches are bracketed by events
+    bool one_stream = false;  // jsrt.h JSRT_EVENTS_ONE_STREAM: no overlapping batch streams
     uint32_t batches = 0; // (pixels x samples) batches completed
     uint32_t attempts = 0; // frame attempts (a poisoned frame is redone)
     bool on(int k) const { return (mask >> k) & 1u; }
