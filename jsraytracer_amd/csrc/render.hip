@@ -417,6 +417,17 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     if ((size_t)npix > max_paths) npix = (uint32_t)(max_paths & ~(size_t)63);
     else nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)A.spp));
     if (A.samples_per_batch > 0) nsb = std::min<uint32_t>(nsb, (uint32_t)A.samples_per_batch);
+    // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
+    const char *pe = getenv("JSRT_PERSIST");
+    const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
+    // A frame that fits one batch of 32 M paths or more (a rank's columns of a two-GPU render) is cut into
+    // two batches of half the samples, so that they run on the two batch streams (below): cornell at
+    // 1024^2 x 32 +3.6 %; at 16 M paths the halves lose 5 % (profiles/r03_s18_ab.txt s28), so smaller frames
+    // stay whole.  JSRT_SPLIT_FRAME=0 keeps one batch.
+    const char *sf = getenv("JSRT_SPLIT_FRAME");
+    if (!persist && !(sf && sf[0] == '0') && npix == npix_total && nsb == (uint32_t)A.spp && A.spp >= 2 &&
+        (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << 25))
+        nsb = (uint32_t)((A.spp + 1) / 2);
     // Chain schedule when no node can have two children: depth x paths node records, nothing can
     // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all
     // levels of a batch (one level may hold half of it), compacted level by level.  Its launches
@@ -446,9 +457,6 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     // (A/B on MI355X, profiles/r03_s18_ab.txt: cornell +12.5 %, the dragon +2.6 %, bunny +0.6 %; two
     // persistent SDF marches side by side lose 1 %, so SDF scenes with persistent casts run on one
     // stream.)  The twin pool is allocated only if it fits; otherwise the frame runs on one pool.
-    // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
-    const char *pe = getenv("JSRT_PERSIST");
-    const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
     const uint64_t nbatches = (uint64_t)((A.spp + nsb - 1) / nsb) * ((npix_total + npix - 1) / npix);
     // A render that asks for its launches' own times (JSRT_EVENTS_ONE_STREAM) runs on one stream: a
     // launch's event interval is only its own time when no other batch's kernels share the CUs.
