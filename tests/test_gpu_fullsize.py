@@ -21,12 +21,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOL = 1e-5
 
-# (config, scene, W, H, spp, depth, column stride): bench.py CONFIGS at full size
+# (config, scene, W, H, spp, depth, column stride, first column): bench.py CONFIGS at full size; the
+# columns start off the 16-column tile and 8-pixel patch boundaries
 CASES = [
-    ("cornell_box_path", "cornell_box_path", 1024, 1024, 64, 8, 128),
-    ("bunny", "bunny", 1920, 1080, 16, 4, 128),
-    ("SDF_Menger", "SDF_Menger", 1024, 1024, 32, 4, 128),
-    ("dragon", "dragon", 4096, 4096, 256, 4, 1024),
+    ("cornell_box_path", "cornell_box_path", 1024, 1024, 64, 8, 64, 37),
+    ("bunny", "bunny", 1920, 1080, 16, 4, 64, 37),
+    ("SDF_Menger", "SDF_Menger", 1024, 1024, 32, 4, 64, 37),
+    ("dragon", "dragon", 4096, 4096, 256, 4, 1024, 0),
 ]
 
 
@@ -39,13 +40,13 @@ def _blob(scene):
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_gpu_full_frame_matches_oracle_columns(case):
     import jsraytracer_amd as jr
-    name, scene, W, H, spp, depth, stride = case
+    name, scene, W, H, spp, depth, stride, first = case
     blob = _blob(scene)
     sc = jr.Scene(blob, device=0)
     rgba, colors, st = sc.render(W, H, spp, depth, 1, 1)
     assert st["samples"] == W * H * spp
-    ocol, orgba, ost = pyoracle.render(blob, W, H, spp, depth, 1, 1, 0, stride)
-    cols = list(range(0, W, stride))
+    ocol, orgba, ost = pyoracle.render(blob, W, H, spp, depth, 1, 1, first, stride)
+    cols = list(range(first, W, stride))
     assert ost["samples"] == len(cols) * H * spp
     bad = (rgba[:, cols] != orgba[:, cols]).any(-1)
     assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.size} RGBA8 pixels differ"
