@@ -65,8 +65,13 @@ __device__ __forceinline__ void dd_mul(double ah, double al, double bh, double b
 // of OCML's general pow for the Phong exponents the reference scenes use (10, 100).
 __device__ __forceinline__ double pow_int_dd(double x, int n) {
     double bh = x, bl = 0.0, rh = 1.0, rl = 0.0;
+    bool first = true;  // the first factor is copied, not multiplied into (1, 0): dd_mul's outputs are
+                        // normalised, so 1 x (bh, bl) would return (bh, bl) unchanged
     for (;;) {
-        if (n & 1) dd_mul(rh, rl, bh, bl, rh, rl);
+        if (n & 1) {
+            if (first) { rh = bh; rl = bl; first = false; }
+            else dd_mul(rh, rl, bh, bl, rh, rl);
+        }
         n >>= 1;
         if (!n) break;
         dd_mul(bh, bl, bh, bl, bh, bl);
