@@ -14,8 +14,8 @@
 #include "device_common.h"
 #include "render_kernel.h"
 
-#ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade (register budget)
-#define JSRT_SHADE_OCC 2
+#ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade: 4 (SDF 167 -> 128 VGPRs) = Menger +5 %, r03_s34
+#define JSRT_SHADE_OCC 4
 #endif
 #ifndef JSRT_SHADE_OCC_FLAT  // analytic profile: 5 waves (95 VGPRs, 8 spilled) beat 4 (105): cornell +2.4 %, r03_s14
 #define JSRT_SHADE_OCC_FLAT 5
@@ -29,6 +29,9 @@
 #endif
 #ifndef JSRT_EXTEND_OCC
 #define JSRT_EXTEND_OCC 5
+#endif
+#ifndef JSRT_MARCH_OCC  // min waves per SIMD of the persistent SDF marches (k_extend_q, k_shadow_cast)
+#define JSRT_MARCH_OCC 1
 #endif
 #ifndef JSRT_EXTEND_OCC_FLAT  // analytic profile: 6 fits without spills (cornell +1 %, r02_s20)
 #define JSRT_EXTEND_OCC_FLAT 6
@@ -910,7 +913,7 @@ struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
 };
 
 template <int PF, bool CHAIN, bool FO>
-__global__ __launch_bounds__(256) void k_extend_q(DScene S, WArgs W, int L, double minD) {
+__global__ __launch_bounds__(256, JSRT_MARCH_OCC) void k_extend_q(DScene S, WArgs W, int L, double minD) {
     uint32_t count = W.npaths, base = 0;
     if (!CHAIN) {
         const LevelRange R = level_range(W, L);
@@ -963,7 +966,7 @@ __global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
 }
 
 template <int PF, bool CHAIN, bool FO>
-__global__ __launch_bounds__(256) void k_shadow_cast(DScene S, WArgs W, int L) {
+__global__ __launch_bounds__(256, JSRT_MARCH_OCC) void k_shadow_cast(DScene S, WArgs W, int L) {
     uint32_t count = W.npaths;
     if (!CHAIN) count = level_range(W, L).count;
     ShadowSrc src{W};
