@@ -135,6 +135,15 @@ __host__ __device__ inline double to_precision8(double v) {
         double res;
         if (k2 >= 0) {
             res = n * pow10_exact(k2);  // k2 <= 0 here: e10 <= 7
+#ifdef JSRT_RECIP_PARSE
+        } else if (-k2 >= 7 && -k2 <= 9) {  // the SDF repetition range: RN(n / 10^m) as RN(n * RN(10^-m)) plus
+            // one fma-exact remainder correction, bit-identical to the division for every 8-digit n and
+            // m in 1..22 (tests/test_js_number.py::test_reciprocal_parse_exhaustive)
+            const double R = -k2 == 7 ? 1e-7 : (-k2 == 8 ? 1e-8 : 1e-9);
+            const double P = -k2 == 7 ? 1e7 : (-k2 == 8 ? 1e8 : 1e9);
+            const double q0 = n * R;
+            res = fma(fma(-q0, P, n), R, q0);
+#endif
         } else if (-k2 <= 22) {
             res = n / pow10_exact(-k2);
         } else {  // n / (1e22 * B): quotient and exact remainders, one final rounding
