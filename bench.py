@@ -167,6 +167,24 @@ def parity(image, colors, ref):
     return out
 
 
+# environment knobs that change the library's schedule (A/B experiments, tools/ab_env.sh) or swap the library
+# itself (JSRT_LIB: a variant build); JSRT_BENCH_BACKEND only picks the multi-rank gather backend
+NOT_KNOBS = ("JSRT_BENCH_BACKEND",)
+
+
+def knobs():
+    """Every JSRT_* environment variable set for this run that can change what is timed."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("JSRT_") and k not in NOT_KNOBS}
+
+
+def exit_status(par):
+    """Process exit status after the bench line: non-zero when the timed frame failed its parity check."""
+    if par is not None and not par["pass"]:
+        print(f"bench: PARITY FAILURE against the oracle: {par}", file=sys.stderr)
+        return 3
+    return 0
+
+
 def load_pmc(config, kname):
     """Counters of kernel `kname` (any template instance: one kernel profile runs per scene)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -261,7 +279,12 @@ def main():
                          "events and one instrumented one-stream step follows them")
     ap.add_argument("--spp", type=int, default=0, help="profiling only: override the config's spp (same launch "
                     "shapes, fewer batches); a bench line with it is not the config's number")
+    ap.add_argument("--ab", action="store_true", help="allow JSRT_* environment knobs / JSRT_LIB variants (A/B runs; "
+                    "the line records them under `knobs`)")
     args = ap.parse_args()
+    if knobs() and not args.ab:
+        print(f"bench: refusing to time with library knobs set {knobs()} (A/B only: pass --ab)", file=sys.stderr)
+        sys.exit(2)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
@@ -390,6 +413,7 @@ def main():
                        "col_block": cb, "headline": args.config == HEADLINE and args.spp == 0,
                        "gather_backend": backend if world > 1 else None},
             "roofline": roof, "cpu_baseline": cpu, "parity": par,
+            "build_id": jr._native.build_id(), "knobs": knobs(),
             "kernel_ms_per_step": kernel_ms,
             "scene_build_s": round(t_build, 3), "scene_upload_s": round(t_upload, 3),
             "events_lost": {"timed": sum(x["events_lost"] for x in stats), "stage_split": st_after["events_lost"]},
@@ -404,9 +428,8 @@ def main():
         sys.stdout.flush()
     if world > 1:
         dist.destroy_process_group()
-    if par is not None and not par["pass"]:
-        print(f"bench: PARITY FAILURE against the oracle: {par}", file=sys.stderr)
+    return exit_status(par)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define JSRT_ABI_VERSION 2
+#define JSRT_ABI_VERSION 3
 
 typedef struct jsrt_scene jsrt_scene;
 
@@ -119,6 +119,9 @@ int32_t jsrt_owned_columns(int32_t width, int32_t x_offset, int32_t x_delt, int3
 
 const char *jsrt_last_error(void);
 int32_t jsrt_abi_version(void);
+/* Identity of this build: a hash of the sources, headers, compiler flags and defines it was compiled
+ * from (jsraytracer_amd/build.py build_id).  Hosts compare it with the tree they run from. */
+const char *jsrt_build_id(void);
 /* Device count visible to HIP (0 without a GPU); never initialises a context it does not need. */
 int32_t jsrt_device_count(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JSRT_LIB") or os.path.join(HERE, "_build", "libjsrt.so")  # JSRT_LIB: A/B builds
-ABI_VERSION = 2  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
+ABI_VERSION = 3  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
 EVENTS_ONE_STREAM = 0x40000000  # include/jsrt.h JSRT_EVENTS_ONE_STREAM (a Params.stage_events flag)
 
 
@@ -48,7 +48,7 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_v
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_cast",
            "jsrt_material_data", "jsrt_sdf_distance", "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version",
-           "jsrt_device_count"]
+           "jsrt_device_count", "jsrt_build_id"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 # exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
@@ -86,6 +86,18 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise JsrtError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__; __graft_entry__.build()'`")
     L = ctypes.CDLL(LIB_PATH)
+    # a stale library (the .so travels to the GPU box on its own) would write past Stats or misread it:
+    # the ABI version first, before any other symbol is bound (a missing one would raise AttributeError)
+    L.jsrt_abi_version.restype = ctypes.c_int32
+    if L.jsrt_abi_version() != ABI_VERSION:
+        raise JsrtError(f"{LIB_PATH}: ABI {L.jsrt_abi_version()}, these bindings expect {ABI_VERSION}: rebuild it")
+    L.jsrt_build_id.restype = ctypes.c_char_p
+    built = L.jsrt_build_id().decode()
+    if not os.environ.get("JSRT_LIB"):  # A/B variants (JSRT_LIB) carry their own defines, hence their own id
+        from . import build as _b
+        want = _b.build_id()
+        if built != want:
+            raise JsrtError(f"{LIB_PATH} was built from other sources (build id {built}, this tree {want}): rebuild it")
     L.jsrt_scene_create.restype = ctypes.c_int
     L.jsrt_scene_create.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]
     L.jsrt_scene_destroy.restype = None
@@ -106,7 +118,6 @@ def lib():
     L.jsrt_owned_columns.restype = ctypes.c_int32
     L.jsrt_owned_columns.argtypes = [ctypes.c_int32] * 4
     L.jsrt_last_error.restype = ctypes.c_char_p
-    L.jsrt_abi_version.restype = ctypes.c_int32
     L.jsrt_device_count.restype = ctypes.c_int32
     L.jsrt_blob_attach_obj.restype = ctypes.c_int
     L.jsrt_blob_attach_obj.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
@@ -123,11 +134,13 @@ def lib():
                                       ctypes.POINTER(JsonInfo)]
     L.jsrt_blob_free.restype = None
     L.jsrt_blob_free.argtypes = [ctypes.c_void_p]
-    # a stale library (the .so travels to the GPU box on its own) would write past Stats or misread it
-    if L.jsrt_abi_version() != ABI_VERSION:
-        raise JsrtError(f"{LIB_PATH}: ABI {L.jsrt_abi_version()}, these bindings expect {ABI_VERSION}: rebuild it")
     _lib = L
     return L
+
+
+def build_id():
+    """The build id embedded in the loaded library (hash of its sources, flags and defines)."""
+    return lib().jsrt_build_id().decode()
 
 
 def last_error():

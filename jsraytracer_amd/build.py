@@ -3,6 +3,7 @@
 The level kernels are compiled once per kernel profile (render_pf.hip with -DJSRT_PF=..., see
 csrc/render_levels.h) as separate objects, all objects in parallel.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -45,6 +46,34 @@ def _path(f):
     return os.path.join(INCLUDE, f) if f in PUBLIC else os.path.join(CSRC, f)
 
 
+def build_id(defines=()):
+    """Identity of a library build: a hash of every source and header it is compiled from, the compiler
+    flags and the variant defines.  Embedded in libjsrt.so (jsrt_build_id) and recomputed from the tree by
+    _native.lib(), which refuses a library built from other sources (the .so travels to the GPU box on its
+    own, so a stale one would otherwise run silently)."""
+    h = hashlib.sha256()
+    files = sorted({src for _, src, _, _ in UNITS} | {d for _, _, _, deps in UNITS for d in deps})
+    for f in files:
+        h.update(f.encode() + b"\0")
+        with open(_path(f), "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join(FLAGS + NO_MLICM + [ARCH] + list(defines)).encode())
+    return h.hexdigest()[:16]
+
+
+def _id_file(lib):
+    return lib + ".id"
+
+
+def _write_id_unit(bid, tag):
+    """A one-function translation unit exporting the build id (compiled into the library at link time)."""
+    src = os.path.join(OUT, f"build_id{tag}.cpp")
+    with open(src, "w") as f:
+        f.write('extern "C" const char *jsrt_build_id(void) { return "%s"; }\n' % bid)
+    return src
+
+
 def _newer(target, deps):
     if not os.path.exists(target):
         return True
@@ -62,8 +91,13 @@ def _deps(src, deps):
 
 def _stale():
     objs = [_obj(stem) for stem, _, _, _ in UNITS]
-    if os.path.exists(LIB) and not any(os.path.exists(o) for o in objs):
-        return False  # a prebuilt library shipped without its objects (the GPU box's snapshot): use it
+    if not os.path.exists(LIB) or not os.path.exists(_id_file(LIB)):
+        return True
+    with open(_id_file(LIB)) as f:
+        if f.read().strip() != build_id():
+            return True  # built from other sources (mtimes do not survive every copy; the id does)
+    if not any(os.path.exists(o) for o in objs):
+        return False  # a prebuilt library shipped without its objects (the GPU box's snapshot), same id: use it
     return any(_newer(_obj(stem), _deps(src, deps)) for stem, src, _, deps in UNITS) or _newer(LIB, objs)
 
 
@@ -104,14 +138,20 @@ def _build_locked(force, verbose, variant, defines, profiles):
         subprocess.run(cmd, check=True)
         os.replace(o + ".tmp", o)
 
+    bid = build_id(defines if variant is not None else ())
+    id_src = _write_id_unit(bid, tag)
+    id_obj = _obj("build_id", tag)
+    jobs.append(([HIPCC] + OBJ_FLAGS + ["-c", id_src, "-o", id_obj + ".tmp"], id_obj))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with ThreadPoolExecutor(workers) as ex:
         list(ex.map(run, jobs))
-    cmd = [HIPCC] + FLAGS + objs + ["-o", lib + ".tmp"]
+    cmd = [HIPCC] + FLAGS + objs + [id_obj, "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(lib + ".tmp", lib)
+    with open(_id_file(lib), "w") as f:
+        f.write(bid + "\n")
     return lib
 
 

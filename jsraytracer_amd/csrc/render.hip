@@ -408,7 +408,8 @@ void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStrea
 }  // namespace
 
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
-                        size_t max_paths, const std::function<bool(int, double, bool)> &progress) {
+                        size_t max_paths, const std::function<bool(int, double, bool)> &progress,
+                        const std::function<bool()> &due) {
     if (!A.accum) return hipErrorInvalidValue;
     const uint32_t npix_total = (uint32_t)A.patches * 64u;
     if (ns > 4) max_paths = max_paths * 4 / (size_t)ns;  // the per-sample hand-off scales with ns
@@ -427,7 +428,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     const char *sf = getenv("JSRT_SPLIT_FRAME");
     if (!persist && !(sf && sf[0] == '0') && npix == npix_total && nsb == (uint32_t)A.spp && A.spp >= 2 &&
         (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << 25))
-        nsb = (uint32_t)((A.spp + 1) / 2);
+        nsb = (uint32_t)((A.spp + 1) / 2);  // odd spp: halves of (spp + 1) / 2 and (spp - 1) / 2 samples
     // Chain schedule when no node can have two children: depth x paths node records, nothing can
     // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all
     // levels of a batch (one level may hold half of it), compacted level by level.  Its launches
@@ -462,9 +463,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     // launch's event interval is only its own time when no other batch's kernels share the CUs.
     const bool timed_launches = kt && kt->one_stream;
     const char *de = getenv("JSRT_DUAL");
-    // two streams need two full batches: a frame of one full batch and a small remainder (bunny: 32 M + 1.2 M
-    // paths) has nothing to overlap
-    const bool two_full = (uint64_t)npix_total * (uint64_t)A.spp >= 2 * (uint64_t)npix * nsb;
+    // two streams need two batches of comparable size: a frame of one full batch and a small remainder
+    // (bunny: 32 M + 1.2 M paths) has nothing to overlap; a split frame of odd spp (nsb and nsb - 1 samples)
+    // does
+    const bool two_full = (uint64_t)npix_total * (uint64_t)A.spp >= 2 * (uint64_t)npix * nsb - (uint64_t)npix;
     bool dual = !timed_launches && nbatches > 1 && (de ? de[0] == '1' : (!persist && two_full));
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_acc[2] = {nullptr, nullptr};
     auto release_events = [&] {
@@ -620,9 +622,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 if ((e = hipGetLastError()) != hipSuccess) break;
                 done += (uint64_t)Wb.npix * nb;
                 if (kt) ++kt->batches;
-                if (progress && A.kind != JSRT_RENDERER_INCREMENTAL) {
+                if (progress && A.kind != JSRT_RENDERER_INCREMENTAL && (!due || due())) {
                     // Simple / RandomMultisampling report {pass: 0, completion: pixels done / total} from
-                    // inside their pixel loop (renderers.js:28-37): here after every batch
+                    // inside their pixel loop (renderers.js:28-37): here after a batch, when a callback is
+                    // due (the host's timelimit clock is checked first: no sync otherwise)
                     if ((e = read_flags()) != hipSuccess) break;
                     const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                     const double c = (double)done / (double)total;
@@ -644,7 +647,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     }
                 }
             }
-            if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL) {  // completion of finished work: wait for the pass
+            if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL && (!due || due())) {  // wait for the pass
                 if ((e = read_flags()) != hipSuccess) break;
                 const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                 const double c = (double)done / (double)total;

@@ -147,8 +147,11 @@ struct KernelTimes {
 // progress(pass, completion, clean) -> false aborts.  It is called after samples [0, pass] of every
 // pixel are in A.accum and the stream is idle; clean = no batch so far outgrew its pool / bounds
 // (so the accumulator holds exactly the reference's sums and render_preview may publish it).
+// due (nullable): whether a callback is due now (the host's timelimit clock); the frame syncs and calls
+// progress only then.
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
-                        size_t max_paths, const std::function<bool(int, double, bool)> &progress);
+                        size_t max_paths, const std::function<bool(int, double, bool)> &progress,
+                        const std::function<bool()> &due = nullptr);
 
 // Device bytes of the batch state per path of a batch (Wavefront::reserve for the schedule and pool
 // render_frame picks for this scene): caps the default batch size.

@@ -851,6 +851,9 @@ struct Loader {
         S.cam.sensor = C.sensor_size;
         S.cam.kind = (int32_t)C.kind;
 
+        // the shadow hand-off packs the material index into 23 bits beside the kr flag (render_levels.h
+        // store_hand: mat << 8 | mask | HAND_KR)
+        if (B.n_mat >= (1u << 23)) fail("more than 2^23 materials");
         for (uint32_t i = 0; i < B.n_mat; ++i) {
             const jsrt_rec_material &M = B.mat[i];
             if (M.kind < JSRT_MAT_PHONG || M.kind > JSRT_MAT_TRANSPARENT) fail("unsupported material kind");

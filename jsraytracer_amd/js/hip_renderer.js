@@ -20,7 +20,7 @@
  */
 const path = require("path");
 
-const ABI_VERSION = 2;  // include/jsrt.h JSRT_ABI_VERSION this wrapper is written against
+const ABI_VERSION = 3;  // include/jsrt.h JSRT_ABI_VERSION this wrapper is written against
 let _addon = null;
 function addon() {
     if (_addon) return _addon;

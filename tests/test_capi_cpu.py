@@ -48,7 +48,7 @@ def test_library_is_gfx950(lib):
 
 
 def test_abi_version_and_helpers(lib):
-    assert lib.jsrt_abi_version() == 2
+    assert lib.jsrt_abi_version() == 3
     from jsraytracer_amd import owned_columns
     assert owned_columns(10, 0, 1) == 10
     assert owned_columns(10, 1, 3) == 3            # 1, 4, 7
@@ -72,3 +72,49 @@ def test_scene_header_reader():
     from oracle import pyoracle
     h = jr.scene_header(pyoracle.golden_scene("cornell_box_path"))
     assert h == {"kind": 1, "spp": 128, "max_depth": 8, "width": 600, "height": 600}
+
+
+def test_build_id_ties_library_to_tree(lib, tmp_path):
+    """jsrt_build_id is the hash of the sources, flags and defines the library was built from; the
+    bindings refuse a library whose id is not this tree's (a stale .so shipped to the GPU box)."""
+    from jsraytracer_amd import _native
+    from jsraytracer_amd import build as jb
+    assert lib.jsrt_build_id().decode() == jb.build_id() == _native.build_id()
+    assert jb.build_id(["-DJSRT_X=1"]) != jb.build_id()  # a variant's defines change it
+    # a copy of one source with an edit: the id of that tree differs
+    src = open(os.path.join(jb.CSRC, "render.hip")).read()
+    old = jb.CSRC
+    try:
+        d = tmp_path / "csrc"
+        d.mkdir()
+        for f in os.listdir(old):
+            (d / f).write_text(open(os.path.join(old, f)).read())
+        (d / "render.hip").write_text(src + "\n// edit\n")
+        jb.CSRC = str(d)
+        assert jb.build_id() != _native.build_id()
+    finally:
+        jb.CSRC = old
+
+
+def test_bench_exits_nonzero_on_parity_failure():
+    """bench.py turns a timed frame that differs from the oracle into a non-zero exit status (the line is
+    still printed, with parity.pass false), and refuses to time with JSRT_* knobs set unless --ab."""
+    import numpy as np
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    H, W = 8, 12
+    rng = np.random.default_rng(1)
+    orgba = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+    ocol = rng.random((H, W, 4), dtype=np.float32)
+    ok = bench.parity(orgba.copy(), ocol.copy(), (ocol, orgba, 1, 3))
+    assert ok["pass"] and bench.exit_status(ok) == 0
+    broken = orgba.copy()
+    broken[5, 4, 1] ^= 1  # one byte of one owned column (1, 4, 7, 10)
+    bad = bench.parity(broken, ocol.copy(), (ocol, orgba, 1, 3))
+    assert not bad["pass"] and bad["rgba8_pixels_differing"] == 1 and bench.exit_status(bad) != 0
+    assert bench.exit_status(None) == 0  # --no-parity
+    env = dict(os.environ, JSRT_DUAL="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "--ab" in r.stderr and not r.stdout

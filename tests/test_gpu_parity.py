@@ -118,17 +118,23 @@ def test_gpu_progress_callback(jr):
 @pytest.mark.parametrize("kind,spp", [(0, 1), (2, 3)])
 def test_gpu_progress_simple_and_random(jr, kind, spp):
     """renderers.js:28-37: SimpleRenderer / RandomMultisamplingRenderer report {pass: 0, completion:
-    pixels done / total} from inside their pixel loop.  Through HipRenderer with a tiny timelimit they
-    fire at least one callback, pass 0, completion increasing in (0, 1), and the image equals the
-    render without a callback."""
+    pixels done / total} from inside their pixel loop; here after a batch when a callback is due.  A frame
+    of several batches with a tiny timelimit fires callbacks with pass 0 and completion increasing in
+    (0, 1); the image equals the render without a callback, through Scene.render and HipRenderer (whose
+    48x40 frame is one batch: a callback never reports completion 1)."""
     sc = _scene(jr, "cornell_box_path")
-    img = jr.PixelBuffer(48, 40)
     seen = []
-    jr.HipRenderer(sc, samplesPerPixel=spp, maxRecursionDepth=8, kind=kind, seed=3).render(
-        img, 1e-9, lambda p: seen.append((p["pass"], p["completion"])))
+    got, _, _ = sc.render(48, 40, spp, 8, kind, 3, want_colors=False, max_paths=512,
+                          progress=lambda p, c: seen.append((p, c)), timelimit_ms=1e-6)
     assert seen and all(p == 0 and 0 < c < 1 for p, c in seen)
     assert [c for _, c in seen] == sorted(c for _, c in seen)
     ref, _, _ = sc.render(48, 40, spp, 8, kind, 3, want_colors=False)
+    assert np.array_equal(got, ref)
+    img = jr.PixelBuffer(48, 40)
+    seen2 = []
+    jr.HipRenderer(sc, samplesPerPixel=spp, maxRecursionDepth=8, kind=kind, seed=3).render(
+        img, 1e-9, lambda p: seen2.append((p["pass"], p["completion"])))
+    assert all(p == 0 and 0 < c < 1 for p, c in seen2)
     assert np.array_equal(img.imgdata, ref)
 
 

@@ -9,7 +9,7 @@ TAG=$1; shift
 for CFG in "$@"; do
   timeout -k 10 600 python bench.py --config "$CFG" --steps 3 --warmup 1 > gpurun_out/bench_${TAG}_$CFG.json 2> gpurun_out/bench_${TAG}_$CFG.err || exit $?
   cat gpurun_out/bench_${TAG}_$CFG.json
-  JSRT_DUAL=0 JSRT_SPLIT=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$CFG -o run -- \
-      python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof_${TAG}_$CFG.json 2> gpurun_out/prof_${TAG}_$CFG.err || exit $?
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$CFG -o run -- \
+      python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --events > gpurun_out/bench_prof_${TAG}_$CFG.json 2> gpurun_out/prof_${TAG}_$CFG.err || exit $?
   head -4 gpurun_out/prof_${TAG}_$CFG/run_kernel_stats.csv
 done

@@ -16,6 +16,6 @@ i=0
 for P in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
   i=$((i+1))
   mkdir -p gpurun_out/pmc_$TAG; timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d gpurun_out/pmc_$TAG/p$i -o run -- \
-     python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline --no-parity ${PMC_BENCH_ARGS:-} > gpurun_out/pmc_$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc_$TAG/p$i.log; exit 1; }
+     python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline --no-parity --ab ${PMC_BENCH_ARGS:-} > gpurun_out/pmc_$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc_$TAG/p$i.log; exit 1; }
 done
 python tools/pmc_summary.py gpurun_out/pmc_$TAG --config "$CFG" --merge gpurun_out/pmc_$TAG/pmc_merge.json > gpurun_out/pmc_$TAG/summary.txt && cat gpurun_out/pmc_$TAG/summary.txt
