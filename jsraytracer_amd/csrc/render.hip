@@ -29,7 +29,7 @@ const char *const KT_NAMES[KT_N] = {"k_gen", "k_extend", "k_shade", "k_shadow", 
 // camera rays: one per path q of the batch, sample-major (neighbouring q are neighbouring pixels)
 __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W) {
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-    if (!W.chain && q < LVL_UNDER) W.lvl[q] = q == 0 ? W.npaths : 0u;  // level counts (not the frame flags)
+    if ((!W.chain || W.hybrid) && q < LVL_UNDER) W.lvl[q] = q == 0 ? W.npaths : 0u;  // level counts (not the frame flags)
     if (q >= W.npaths) return;
     int c = 0, py = 0, px = 0;
     const uint32_t pl = q % W.npix, sl = q / W.npix;
@@ -146,12 +146,12 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
     if (!pixel_of(A, W.p0 + pl, c, py, px)) return;
     const size_t oi = (size_t)c * A.H + py;
     F3 acc = f3(A.accum[4 * oi], A.accum[4 * oi + 1], A.accum[4 * oi + 2]);
-    const uint32_t nsb = W.npaths / W.npix, P = W.npaths;
+    const uint32_t nsb = W.npaths / W.npix;
     for (uint32_t sl = 0; sl < nsb; ++sl) {
         const uint32_t q = sl * W.npix + pl;
         F3 v = f3(0, 0, 0);  // World.color(ray, 0) = black
         for (int L = A.max_depth - 1; L >= 0; --L) {
-            const uint32_t i = (uint32_t)L * P + q;
+            const uint32_t i = (uint32_t)L * W.cap + q;
             const float4 nd = W.node[i];
             const uint32_t info = f2u(nd.w);
             if (info & INFO_MISS) {
@@ -167,6 +167,55 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
     A.accum[4 * oi] = acc.x;
     A.accum[4 * oi + 1] = acc.y;
     A.accum[4 * oi + 2] = acc.z;
+}
+
+// hybrid chain: the colour of chain c, which starts at level s, bottom-up over its levels (surface + the
+// first child's contribution -- the chain's own next level -- + the second child's, a side chain's colour
+// in slot[i]; children of the last level are black without a cast), materials.js:277-330
+__device__ __forceinline__ F3 resolve_chain(const RenderArgs &A, const WArgs &W, uint32_t c, int s) {
+    F3 v = f3(0, 0, 0);
+    for (int L = W.endl[c]; L >= s; --L) {
+        const uint32_t i = (uint32_t)L * W.cap + c;
+        const float4 nd = W.node[i];
+        const uint32_t info = f2u(nd.w);
+        if (info & INFO_MISS) {
+            v = f3(nd.x, nd.y, nd.z);
+        } else if (info & INFO_HIT) {
+            const bool last = L == A.max_depth - 1;
+            const int n = (int)((info >> INFO_NCHILD_SHIFT) & 3);
+            F3 col = f3(nd.x, nd.y, nd.z);
+            if (n > 0) col = add_child(W, i, 0, col, last ? f3(0, 0, 0) : v, info);
+            if (n > 1) {
+                const float4 v1 = last ? make_float4(0, 0, 0, 0) : W.slot[i];
+                col = add_child(W, i, 1, col, f3(v1.x, v1.y, v1.z), info);
+            }
+            v = col;
+        }
+    }
+    return v;
+}
+
+// hybrid chain: the side chains that start at level s (ids npaths + [side(< s), side(<= s))), into their
+// parents' second-child slots.  Launched for s = depth - 1 .. 1, so a chain's own side chains are resolved
+// first.
+__global__ __launch_bounds__(256) void k_resolve_side(RenderArgs A, WArgs W, int s) {
+    if (W.lvl[LVL_FLAG]) return;
+    uint32_t lo = W.npaths;
+    for (int j = 1; j < s; ++j) lo += W.lvl[LVL_SIDE + j];
+    const uint32_t c = lo + blockIdx.x * 256 + threadIdx.x;
+    if (c >= lo + W.lvl[LVL_SIDE + s]) return;
+    const F3 v = resolve_chain(A, W, c, s);
+    W.slot[W.parent[c]] = make_float4(v.x, v.y, v.z, 0.0f);
+}
+
+// hybrid chain: every path's colour -> root (k_accum adds them per pixel in sample order)
+__global__ __launch_bounds__(256) void k_resolve_paths(RenderArgs A, WArgs W) {
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= W.npaths || W.lvl[LVL_FLAG]) return;
+    const F3 v = resolve_chain(A, W, q, 0);
+    W.root[3 * q] = v.x;
+    W.root[3 * q + 1] = v.y;
+    W.root[3 * q + 2] = v.z;
 }
 
 __global__ __launch_bounds__(256) void k_final(RenderArgs A, int32_t passes) {
@@ -220,15 +269,20 @@ EventPairs::~EventPairs() {
     for (auto x : e) (void)hipEventDestroy(x);
 }
 
-hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree, size_t shadow) {
+hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t paths, int mode, size_t shadow) {
+    const bool tree = mode == SCHED_TREE, hybrid = mode == SCHED_HYBRID;
     size_t bytes = 0;
     bytes += 8 * need(rays, 4) + need(rays, 8) + 2 * need(rays, 4);  // o d addr key + t + prim ctx
     if (tree) bytes += 2 * need(rays, 4);                            // path parent
+    if (hybrid) bytes += 3 * need(rays, 4) + need(rays, 1);          // parent, live lists, last levels
     bytes += need(nodes, 16) + need(4 * nodes, 16);                  // node + child
-    if (tree) bytes += need(2 * nodes, 16) + need(3 * paths, 4);     // slot + root
+    if (tree) bytes += need(2 * nodes, 16);                          // slot
+    if (hybrid) bytes += need(nodes, 16);                            // slot (second children)
+    if (tree || hybrid) bytes += need(3 * paths, 4);                 // root
     bytes += need(HAND_PLANES * hands, 16) + need(64, 4);            // hand-off + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
-    if (tree) bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);  // buckets
+    if (tree || hybrid)  // buckets
+        bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
     } else {
         if (mem) (void)hipFree(mem);
@@ -246,14 +300,22 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     w.addr = carve<uint32_t>(p, rays); w.key = carve<uint32_t>(p, rays);
     w.t = carve<double>(p, rays); w.prim = carve<int32_t>(p, rays); w.ctx = carve<int32_t>(p, rays);
     if (tree) { w.path = carve<uint32_t>(p, rays); w.parent = carve<uint32_t>(p, rays); }
+    if (hybrid) {
+        w.parent = carve<uint32_t>(p, rays);
+        w.list0 = carve<uint32_t>(p, rays);
+        w.list1 = carve<uint32_t>(p, rays);
+        w.endl = carve<uint8_t>(p, rays);
+    }
     w.node = carve<float4>(p, nodes);
     w.child = carve<float4>(p, 4 * nodes);
-    if (tree) { w.slot = carve<float4>(p, 2 * nodes); w.root = carve<float>(p, 3 * paths); }
+    if (tree) w.slot = carve<float4>(p, 2 * nodes);
+    if (hybrid) w.slot = carve<float4>(p, nodes);
+    if (tree || hybrid) w.root = carve<float>(p, 3 * paths);
     w.hand = carve<float4>(p, HAND_PLANES * hands);
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
-    if (tree) {
+    if (tree || hybrid) {
         w.bkt = carve<uint32_t>(p, MAX_TREE_DEPTH * BKT_LEVEL);
         w.bbase = carve<uint32_t>(p, (hands / 256 + 1) * BKT_N);
         w.brank = carve<uint32_t>(p, rays);
@@ -280,13 +342,27 @@ Wavefront::~Wavefront() {
     if (ev_shadow) (void)hipEventDestroy(ev_shadow);
 }
 
+// The schedule of a scene's frames: chain when no node can have two children; otherwise the hybrid chain
+// (side chains for second children) unless JSRT_HYBRID=0 asks for the tree schedule.
+int schedule_of(const DScene &S) {
+    if (S.max_children <= 1) return SCHED_CHAIN;
+    const char *hy = getenv("JSRT_HYBRID");
+    return (hy && hy[0] == '0') ? SCHED_TREE : SCHED_HYBRID;
+}
+constexpr size_t HYBRID_POOL_FACTOR = 2;  // initial hybrid side-chain slots: paths x factor / 4
+
 size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
     const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = HAND_PLANES * 16;
     const bool persist = (S.profile & PF_SDF) && S.all_roots_prims;
     size_t group = 1;
     while ((int)group < ns && ns <= 64) group *= 2;
-    if (S.max_children <= 1)  // chain: one ray and depth nodes per path
-        return ray + (size_t)std::max(1, max_depth) * node + hand + (persist ? group * 48 : 0);
+    const int sched = schedule_of(S);
+    const size_t depth = (size_t)std::max(1, max_depth);
+    if (sched == SCHED_CHAIN)  // chain: one ray and depth nodes per path
+        return ray + depth * node + hand + (persist ? group * 48 : 0);
+    if (sched == SCHED_HYBRID)  // per chain slot: ray + parent + rank, depth x (node + second-child slot), hand-off
+        return (4 + HYBRID_POOL_FACTOR) * (ray + 17 + depth * (node + 16) + hand + (persist ? group * 48 : 0) +
+                                           BKT_N * 4 / 256) / 4 + 12;
     const size_t pool = 8, level_cap = pool / 2;  // render_frame: pool = 8 x paths, level_cap = pool / 2
     // + the bucketed hand-off's ranks (4 B per pool slot) and block bases (BKT_N words per 256 hand-off slots)
     return pool * (ray + 8 + node + 2 * 16 + 4) + level_cap * (hand + (persist ? group * 48 : 0) + BKT_N * 4 / 256) + 12;
@@ -436,21 +512,27 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     // batch shape) with a margin; a batch that outgrows its pool (LVL_FLAG) or a launch bound
     // (LVL_UNDER) poisons the frame, which is redone with a larger pool / conservative bounds.
     // The frame flags are read once, after the last batch.
-    const bool chain = S.max_children <= 1;
+    // Hybrid chain (branching materials, the default): the chain layout -- ray slot = path, node [L * cap +
+    // slot], no parent / path planes, one bottom-up resolve -- plus a side chain per second child (a slot
+    // appended after the paths, cap = paths + paths x pool_factor / 4).  Its level counts (the side chains
+    // started so far) live on the device; launch bounds, overflow and redo work as for the tree.
+    const int sched = schedule_of(S);
+    const bool hybrid = sched == SCHED_HYBRID, chain = sched != SCHED_TREE, learned = sched != SCHED_CHAIN;
     const int depth = std::max(1, A.max_depth);
     const size_t paths = (size_t)npix * nsb;
     // test knobs: a smaller first pool / tighter learned bounds exercise the frame redo paths
     const char *pf_env = getenv("JSRT_POOL_FACTOR"), *bm_env = getenv("JSRT_BOUND_MARGIN");
     const double margin = bm_env ? atof(bm_env) : 1.25;
     const size_t slack = bm_env ? 0 : 4096;
-    if (!chain && wf.pool_paths != paths) {  // learned pool / bounds are per batch shape
-        wf.pool_factor = pf_env ? std::max(1, atoi(pf_env)) : 8;
+    if (learned && (wf.pool_paths != paths || wf.pool_mode != sched)) {  // learned pool / bounds: per batch shape
+        wf.pool_factor = pf_env ? std::max(1, atoi(pf_env)) : (hybrid ? HYBRID_POOL_FACTOR : 8);
         wf.frac.clear();
         wf.pool_paths = paths;
+        wf.pool_mode = sched;
     }
     hipError_t e = hipSuccess;
-    uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree schedule)
-    if (!chain && (e = hipHostMalloc((void **)&h_lvl, 128 * sizeof(uint32_t), 0)) != hipSuccess) return e;
+    uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree / hybrid schedule)
+    if (learned && (e = hipHostMalloc((void **)&h_lvl, 128 * sizeof(uint32_t), 0)) != hipSuccess) return e;
     // Two batch pools on two streams: consecutive batches alternate between them, so one batch's levels
     // (latency-bound casts, VALU-bound shadow samples, their launch tails) overlap the other's.  Only the
     // accumulation into A.accum is ordered across them -- each batch's k_accum / k_resolve waits for the
@@ -508,19 +590,24 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     double reported = 0;  // completion already reported: a redone frame reports only beyond it
     for (int attempt = 0; e == hipSuccess; ++attempt) {
         if (kt) kt->attempts = (uint32_t)attempt + 1;
-        const size_t pool = chain ? paths : paths * wf.pool_factor, level_cap = chain ? paths : pool / 2;
+        // chain slots (hybrid: paths + side chains, 256-aligned)
+        const size_t cap = hybrid ? ((paths + paths * wf.pool_factor / 4 + 255) & ~(size_t)255) : paths;
+        if (hybrid && cap * (size_t)depth >= ((size_t)1 << 32)) { e = hipErrorOutOfMemory; break; }  // u32 node index
+        const size_t pool = chain ? cap : paths * wf.pool_factor, level_cap = chain ? cap : pool / 2;
         int group = 1;
         if (ns > 1 && ns <= 64)
             while (group < ns) group *= 2;
         // hand-off slots: one per node of a level; level 0 holds all `paths` camera rays, the
         // deeper levels at most level_cap (k_shade poisons the batch before writing past it)
-        const size_t hands = chain ? paths : std::max(level_cap, paths);
+        const size_t hands = chain ? cap : std::max(level_cap, paths);
         const size_t shadow = persist ? hands * (size_t)group : 0;
-        e = chain ? wf.reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
-                  : wf.reserve(pool, pool, hands, paths, true, shadow);
+        auto reserve = [&](Wavefront &w) {
+            return chain ? w.reserve(cap, cap * (size_t)depth, cap, paths, sched, shadow)
+                         : w.reserve(pool, pool, hands, paths, SCHED_TREE, shadow);
+        };
+        e = reserve(wf);
         if (e == hipSuccess && dual) {
-            const hipError_t e2 = chain ? wf.twin->reserve(paths, paths * (size_t)depth, paths, 0, false, shadow)
-                                        : wf.twin->reserve(pool, pool, hands, paths, true, shadow);
+            const hipError_t e2 = reserve(*wf.twin);
             if (e2 == hipErrorOutOfMemory) {  // no room for a second pool: one pool, one stream
                 (void)hipGetLastError();
                 wf.twin->release();
@@ -535,17 +622,19 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         W.ns = ns;
         W.group = group;
         W.chain = chain ? 1 : 0;
+        W.hybrid = hybrid ? 1 : 0;
+        W.cap = (uint32_t)cap;
         // shadow hand-off bucketed by hit primitive (<= BKT_N buckets of consecutive primitives)
         const char *be = getenv("JSRT_BUCKET");
         int shift = 0;
         while (S.n_prims > 0 && ((S.n_prims - 1) >> shift) >= BKT_N) ++shift;
-        W.bucket = (!chain && !persist && S.n_prims > 0 && ns > 0 && ns <= 64 && !(be && be[0] == '0')) ? shift + 1 : 0;
+        W.bucket = (learned && !persist && S.n_prims > 0 && ns > 0 && ns <= 64 && !(be && be[0] == '0')) ? shift + 1 : 0;
         W.pool = pool;
         W.level_cap = level_cap;
         // children grouped by direction octant where the next cast walks a BVH (A/B on MI355X,
         // profiles/r03_s3_ab.txt: bunny +5.5 %; cornell -0.8 %, its keyed append costing k_shade 3 ms)
         const char *cs = getenv("JSRT_CHILD_SORT");
-        W.child_sort = cs ? (cs[0] == '1') : ((S.profile & PF_BVH) != 0);
+        W.child_sort = !chain && (cs ? (cs[0] == '1') : ((S.profile & PF_BVH) != 0));  // (tree appends only)
         // hand-off buckets keyed by the hit point's grid cell, with per-cell shadow-root masks, for flat
         // scenes (cornell +1.5 %, r03_s15); by hit primitive (runs of consecutive triangles) for meshes,
         // where the BVH and not the root loop carries the shadow casts (bunny +-0.2 %, r03_s6)
@@ -560,19 +649,20 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             W2.prim = t.prim; W2.ctx = t.ctx; W2.node = t.node; W2.child = t.child; W2.slot = t.slot;
             W2.hand = t.hand; W2.root = t.root; W2.lvl = t.lvl; W2.qctr = t.qctr; W2.sray = t.sray;
             W2.scol = t.scol; W2.bkt = t.bkt; W2.bbase = t.bbase; W2.brank = t.brank;
+            W2.list0 = t.list0; W2.list1 = t.list1; W2.endl = t.endl;
         }
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
-        if (!chain && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
+        if (learned && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
         if (dual) {  // the side stream starts after everything enqueued on st so far
             if ((e = hipEventRecord(ev_start, st)) != hipSuccess || (e = hipStreamWaitEvent(st2, ev_start, 0)) != hipSuccess) break;
-            if (!chain && (e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;
+            if (learned && (e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;
         }
         // the frame flags (and, for progress, level counts) of both pools, read back after both streams idle
         auto read_flags = [&]() -> hipError_t {
             hipError_t r;
             if (dual && ((r = hipEventRecord(ev_end, st2)) != hipSuccess || (r = hipStreamWaitEvent(st, ev_end, 0)) != hipSuccess))
                 return r;
-            if (!chain) {
+            if (learned) {
                 if ((r = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
                 if (dual && (r = hipMemcpyAsync(h_lvl + 64, W2.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
                     return r;
@@ -583,6 +673,14 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         uint64_t bi = 0;  // batch index: even batches on (W, st), odd ones on (W2, st2)
         auto bounds = [&](uint32_t np) {  // per-level launch bound of a batch of np paths
             std::vector<size_t> b(depth, 0);
+            if (hybrid) {  // level L: its live chains (<= cap)
+                for (int L = 0; L < A.max_depth; ++L) {
+                    b[L] = L == 0 ? np : cap;
+                    if (L > 0 && !conservative && L < (int)wf.frac.size())
+                        b[L] = std::min(cap, (size_t)((double)np * wf.frac[L] * margin) + slack);
+                }
+                return b;
+            }
             size_t ub = np;
             for (int L = 0; L < A.max_depth && ub > 0; ++L) {
                 b[L] = ub;
@@ -605,7 +703,8 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 Wb.npix = std::min(npix, npix_total - p0);
                 Wb.s0 = s0;
                 Wb.npaths = Wb.npix * nb;
-                const std::vector<size_t> bound = chain ? std::vector<size_t>() : bounds(Wb.npaths);
+                Wb.cap = hybrid ? (uint32_t)cap : Wb.npaths;
+                const std::vector<size_t> bound = learned ? bounds(Wb.npaths) : std::vector<size_t>();
                 BatchSync sync;
                 if (dual) {
                     sync.wait = bi > 0 ? ev_acc[(bi - 1) & 1] : nullptr;
@@ -627,14 +726,14 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     // inside their pixel loop (renderers.js:28-37): here after a batch, when a callback is
                     // due (the host's timelimit clock is checked first: no sync otherwise)
                     if ((e = read_flags()) != hipSuccess) break;
-                    const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
+                    const bool clean = !learned || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                     const double c = (double)done / (double)total;
                     if (c > reported) {
                         reported = c;
                         if ((stop = !progress(0, c, clean))) break;
                     }
                 }
-                if (!chain && ((wf.frac.empty() && !conservative) || conservative)) {
+                if (learned && ((wf.frac.empty() && !conservative) || conservative)) {
                     // learn the level counts: from the scene's first batch, or -- when that batch was
                     // not representative and a frame had to be redone -- as the maximum over every
                     // batch of the conservative redo, so later frames of this shape are not redone
@@ -649,7 +748,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             }
             if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL && (!due || due())) {  // wait for the pass
                 if ((e = read_flags()) != hipSuccess) break;
-                const bool clean = chain || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
+                const bool clean = !learned || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
                 const double c = (double)done / (double)total;
                 if (c > reported) {
                     reported = c;
@@ -657,14 +756,14 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 }
             }
         }
-        if (e == hipSuccess && dual && chain) {  // st waits for the side stream's batches
+        if (e == hipSuccess && dual && !learned) {  // st waits for the side stream's batches
             if ((e = hipEventRecord(ev_end, st2)) == hipSuccess) e = hipStreamWaitEvent(st, ev_end, 0);
         }
-        if (e != hipSuccess || chain) break;
+        if (e != hipSuccess || !learned) break;
         if ((e = read_flags()) != hipSuccess) break;
         if (!flagged(LVL_FLAG) && !flagged(LVL_UNDER)) break;
         if (flagged(LVL_FLAG)) {  // a batch outgrew the pool: twice the pool, relearn the counts
-            if (paths * wf.pool_factor > ((size_t)1 << 31)) { e = hipErrorOutOfMemory; break; }
+            if (paths * wf.pool_factor > ((size_t)1 << 31) * (hybrid ? 4 : 1)) { e = hipErrorOutOfMemory; break; }
             wf.pool_factor *= 2;
             wf.frac.clear();
         } else {  // a level outgrew its learned bound: redo with the conservative bounds (and relearn)

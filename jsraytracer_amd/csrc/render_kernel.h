@@ -13,6 +13,7 @@ namespace jsrt {
 constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of the breadth-first schedule)
 constexpr int LVL_FLAG = 63;        // WArgs::lvl word set when a batch outgrew its pool (frame redone)
 constexpr int LVL_UNDER = 62;       // WArgs::lvl word set when a level outgrew its launch bound
+constexpr int LVL_SIDE = 16;        // hybrid chain: WArgs::lvl[LVL_SIDE + s] = side chains started at level s
 constexpr int BKT_N = 64;           // buckets of the shadow hand-off (hit primitive >> shift)
 constexpr int BKT_S = 16;           // slices per bucket (block index % BKT_S): spreads the counters' atomics
 constexpr int BKT_K = BKT_N * BKT_S;  // counters per level, key = bucket * BKT_S + slice
@@ -41,7 +42,13 @@ constexpr int INFO_NCHILD_SHIFT = 2;
 
 // Device buffers of one batch.  Two schedules share them (render.hip):
 //   chain (no node has more than one child): ray q of the batch is path q at every level; node
-//         records are level-major [L * npaths + q]; the child ray replaces its parent's ray.
+//         records are level-major [L * cap + q]; the child ray replaces its parent's ray.
+//         hybrid chain (branching materials, W.hybrid): the same, and a node's second child starts a
+//         side chain in a slot appended after the paths (the chains started at level s have the ids
+//         npaths + [side(< s), side(<= s)), side counts lvl[LVL_SIDE + s]).  Level L > 0 visits only its
+//         live chains, listed by k_shade(L - 1) (list[L & 1], lvl[L] entries); a chain's last level is
+//         endl[slot].  A side chain's colour is resolved bottom-up before its parent's and left in
+//         slot[parent node] (k_resolve_side).
 //   tree  (branching materials): rays and nodes share pool slots; level L occupies
 //         [base_L, base_L + count_L) with counts on the device; children are appended.
 struct WArgs {
@@ -50,17 +57,20 @@ struct WArgs {
     uint32_t *addr;    // ray-tree address of the World.color frame this ray opens
     uint32_t *key;     // mix(mix(seed, pixel), sample): RNG key of the path
     uint32_t *path;    // tree: path index in the batch
-    uint32_t *parent;  // tree: child slot 2 * parent + j, NO_PARENT (camera ray) or DEAD_RAY
+    uint32_t *parent;  // tree: child slot 2 * parent + j, NO_PARENT (camera ray) or DEAD_RAY; hybrid chain:
+                       // [side chain] its branching parent's node index
     double *t;         // closest hit
     int32_t *prim, *ctx;  // prim: hit primitive, -1 miss / to trace, NO_RAY no ray
     // nodes
     float4 *node;      // [i]: {surface colour (the ambient until k_shadow adds the lights), info}
     // record planes (plane stride nstride / hstride): every access is one coalesced 16-B load per lane
     float4 *child;     // [(2 * j + part) * nstride + i]: part 0 {col.xyz, w.x}, part 1 {w.y, w.z, k (f64)}
-    float4 *slot;      // tree: [j * nstride + i] the child's colour
+    float4 *slot;      // tree: [j * nstride + i] the child's colour; hybrid chain: [i] the second child's
     float4 *hand;      // [k * hstride + h], k < 6: shadow hand-off of a lit node (h: path / level index, render_levels.h store_hand)
     float *root;       // tree: [3 * path] root colours
     uint32_t *lvl;     // tree: [L] ray count of level L; [LVL_FLAG] overflow flag
+    uint32_t *list0, *list1;  // hybrid chain: the live chain slots of odd (list1) / even (list0) levels > 0
+    uint8_t *endl;     // hybrid chain: [slot] the chain's last level
     // persistent casts (SDF scenes, render.hip k_extend_q / k_shadow_*): work counters per level
     // ([L] extend, [32 + L] shadow) and the shadow rays of the light samples ([e] = k_shadow lane e)
     uint32_t *qctr;
@@ -77,6 +87,8 @@ struct WArgs {
     int32_t ns;        // light samples per lit node
     int32_t group;     // lanes per node in k_shadow: a power of two >= ns (<= 64), or 1 (serial)
     int32_t chain;     // schedule
+    int32_t hybrid;    // chain schedule with side chains (level counts on the device)
+    uint32_t cap;      // chain schedule: slots per level (node [L * cap + slot]); npaths without side chains
     int32_t bucket;    // tree schedule: 0, or 1 + shift: k_shadow reads lit nodes bucketed by hit primitive >> shift (bkt)
     int32_t child_sort; // tree schedule: k_shade appends a block's children grouped by direction octant
     int32_t bucket_grid; // bucketed hand-off keyed by the hit point's grid cell (DScene::grid_*), not the primitive
@@ -105,19 +117,23 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     // this pool's k_shadow stream and its two ordering events (BatchSync::aux), created on first use
     hipStream_t aux = nullptr;
     hipEvent_t ev_shade = nullptr, ev_shadow = nullptr;
-    // tree schedule, learned per scene and batch shape: pool size (x paths) and level counts
+    // tree / hybrid chain schedule, learned per scene, batch shape and schedule: pool size (tree: x paths;
+    // hybrid: paths + paths x pool_factor / 4 chain slots) and level counts
     size_t pool_paths = 0, pool_factor = 8;
+    int pool_mode = -1;
     std::vector<double> frac;  // level L ray count / paths of the first batch
     size_t cap_bytes = 0;
     WArgs args{};
     // rays: ray slots; nodes: node records; hands: hand-off records; paths: root colours
     // shadow: light-sample entries of the persistent shadow casts (0 if unused)
-    hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, bool tree, size_t shadow = 0);
+    // mode: 0 chain, 1 tree, 2 hybrid chain
+    hipError_t reserve(size_t rays, size_t nodes, size_t hands, size_t paths, int mode, size_t shadow = 0);
     void release();  // frees the buffers (the learned pool / bounds stay)
     ~Wavefront();
 };
 
 enum { KT_GEN, KT_EXTEND, KT_SHADE, KT_SHADOW, KT_REDUCE, KT_ACCUM, KT_FINAL, KT_RESOLVE, KT_N };
+constexpr int SCHED_CHAIN = 0, SCHED_TREE = 1, SCHED_HYBRID = 2;
 extern const char *const KT_NAMES[KT_N];
 
 struct EventPairs {  // reusable HIP events bracketing every launch of one kernel kind

@@ -79,6 +79,37 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
+// Two block-aggregated appends at once (one atomic per block on each counter): n0 (0..2) entries on c0 and
+// n1 (0..1) on c1.  Every thread of the block must call it; o0 / o1 = this thread's first offsets.
+__device__ __forceinline__ void block_append2(uint32_t *c0, int n0, uint32_t *c1, int n1, uint32_t &o0, uint32_t &o1) {
+    constexpr int NW = 256 / 64;
+    __shared__ uint32_t s0[NW + 1], s1[NW + 1];
+    const uint64_t a1 = __ballot(n0 >= 1), a2 = __ballot(n0 >= 2), b1 = __ballot(n1 >= 1);
+    const int lane = (int)__lane_id(), wid = (int)(threadIdx.x >> 6);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t p0 = (uint32_t)(__popcll(a1 & lt) + __popcll(a2 & lt)), p1 = (uint32_t)__popcll(b1 & lt);
+    if (lane == 0) {
+        s0[wid] = (uint32_t)(__popcll(a1) + __popcll(a2));
+        s1[wid] = (uint32_t)__popcll(b1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x0 = 0, x1 = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = s0[w], d = s1[w];
+            s0[w] = x0;
+            s1[w] = x1;
+            x0 += c;
+            x1 += d;
+        }
+        s0[NW] = x0 ? atomicAdd(c0, x0) : 0u;
+        s1[NW] = x1 ? atomicAdd(c1, x1) : 0u;
+    }
+    __syncthreads();
+    o0 = s0[NW] + s0[wid] + p0;
+    o1 = s1[NW] + s1[wid] + p1;
+}
+
 // Block-aggregated append with the block's children grouped by a 3-bit key (the direction octant): one
 // atomic per block on the level counter; o0 / o1 = the offsets of this thread's children in the block's
 // range (children of one key contiguous, in no particular order within a key).  Every thread of the
@@ -173,6 +204,19 @@ __device__ __forceinline__ LevelRange level_range(const WArgs &W, int L) {
     uint32_t b = 0;
     for (int j = 0; j < L; ++j) b += W.lvl[j];
     return LevelRange{b, W.lvl[L]};
+}
+// Chain schedule: level L's node records start at L * cap.  It visits count chains: every path (level 0,
+// and every level without side chains), else the hybrid chain's live chains of level L (lvl[L], listed)
+__device__ __forceinline__ LevelRange chain_level(const WArgs &W, int L) {
+    const uint32_t base = (uint32_t)L * W.cap;
+    if (!W.hybrid) return LevelRange{base, W.npaths};
+    if (W.lvl[LVL_FLAG]) return LevelRange{base, 0u};
+    return LevelRange{base, W.lvl[L]};
+}
+// the chain slot of level L's t-th visited chain
+__device__ __forceinline__ uint32_t chain_slot(const WArgs &W, int L, uint32_t t) {
+    if (!W.hybrid || L == 0) return t;
+    return ((L & 1) ? W.list1 : W.list0)[t];
 }
 
 // The material data k_shade hands to k_shadow for one lit node (after getBaseFactors), plus the
@@ -539,6 +583,8 @@ __global__ __launch_bounds__(256) void k_gen(DScene S, RenderArgs A, WArgs W);
 __global__ __launch_bounds__(256) void k_reduce(WArgs W, int L);
 __global__ __launch_bounds__(256) void k_accum(RenderArgs A, WArgs W);
 __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W);
+__global__ __launch_bounds__(256) void k_resolve_side(RenderArgs A, WArgs W, int s);
+__global__ __launch_bounds__(256) void k_resolve_paths(RenderArgs A, WArgs W);
 
 // Grid of a persistent kernel: as many 256-thread blocks as the device keeps resident (occupancy x
 // CUs), never more than the work needs (render.hip).
@@ -568,11 +614,11 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     uint32_t i = t;
     bool live = true;
-    if (CHAIN) {
-        if (t >= W.npaths) return;
-    } else {
-        const LevelRange R = level_range(W, L);
-        if (t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // the launch bound was too small
+    {
+        // chain: ray slot t of the level's live slots; tree: level L's range of the pool
+        const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+        const uint32_t rbase = CHAIN ? 0u : R.base;
+        if ((!CHAIN || W.hybrid) && t == 0 && R.count > gridDim.x * 256u) W.lvl[LVL_UNDER] = 1u;  // launch bound too small
         if (!W.bucket) {
             if (t >= R.count) return;
         } else {  // every wave of a live block reaches the count below
@@ -582,7 +628,8 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
             __syncthreads();
             live = t < R.count;
         }
-        i = R.base + (live ? t : 0u);
+        i = rbase + (live ? t : 0u);
+        if (CHAIN) i = live ? chain_slot(W, L, t) : 0u;
     }
     int hp = -1, b = 0;  // b: the hit's bucket
     if (live && W.prim[i] != NO_RAY) {
@@ -594,13 +641,13 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         hp = h.prim;
         // grid bucket: the cell of the hit point in f32 (within ~1e-6 of material_data.position, which
         // scene_load.cpp shadow_grid's grown cells cover; k_shade reads the bucket back from brank)
-        if (!CHAIN && W.bucket && hp >= 0) {
+        if (W.bucket && hp >= 0) {
             const float tf = (float)h.t;
             b = W.bucket_grid ? grid_cell(S, f3(fmaf(d.x, tf, o.x), fmaf(d.y, tf, o.y), fmaf(d.z, tf, o.z)))
                               : hp >> (W.bucket - 1);
         }
     }
-    if (!CHAIN && W.bucket) {
+    if (W.bucket) {
         // Bucketed hand-off: ranks every lit hit (S.prim_lit: shade_node lights every hit but Solid /
         // Transparent) among the block's hits in its bucket (wave-aggregated LDS atomics); the
         // block's last wave adds the histogram to the level's per-key counters (one global atomic per
@@ -643,20 +690,18 @@ template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
     DScene S, WArgs W, int L, int child_depth) {
     const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
-    uint32_t count = W.npaths, base = 0, next_base = 0;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-        next_base = R.base + R.count;
+    const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+    const uint32_t count = R.count, base = R.base, next_base = CHAIN ? 0u : R.base + R.count;
+    if (!CHAIN || W.hybrid) {
         if (t0 >= count) return;  // block-uniform: every thread of a live block reaches block_append
     } else if (tt >= count) {
         return;
     }
     const bool in = tt < count;
-    const uint32_t q = in ? tt : 0u;                                     // ray slot (chain) / level index (tree)
-    const uint32_t i = CHAIN ? (uint32_t)L * W.npaths + q : base + q;    // node index
-    const uint32_t r = CHAIN ? q : i;                                    // ray index
+    const uint32_t q = in ? tt : 0u;                          // level index
+    const uint32_t slot = CHAIN && in ? chain_slot(W, L, q) : q;  // chain: the chain's slot
+    const uint32_t i = base + (CHAIN ? slot : q);             // node index (chain: L * cap + slot)
+    const uint32_t r = CHAIN ? slot : i;                      // ray index
     int nchild = 0;
     Child ch0, ch1;
     NodeOut out;
@@ -674,9 +719,9 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
         const Hit h{W.t[r], prim, W.ctx[r]};
         nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
-        out.h.node = q;
+        out.h.node = CHAIN ? slot : q;  // (k_shadow: node base + this)
         out.h.mask = (uint32_t)S.grid_cells;  // every root
-        if (!CHAIN && W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
+        if (W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
             const uint32_t br = W.brank[r];      // bucket << 16 | rank in the block's bucket
             const int b = (int)(br >> 16);
             const uint32_t *B = W.bkt + (size_t)L * BKT_LEVEL;
@@ -689,7 +734,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     // W.child_sort: a block's children grouped by direction octant, so a wave of the next level's k_extend
     // casts rays of one or two octants that walk the same BVH subtrees (WArgs::child_sort)
     uint32_t co[2] = {0u, 1u};  // offsets of the children from `at`
-    uint32_t at = 0;
+    uint32_t at = 0, side_at = 0;
     if (!CHAIN) {
         const int nc = child_depth > 0 ? nchild : 0;
         if (W.child_sort)  // (kernel argument: block-uniform, every thread reaches the barriers)
@@ -697,10 +742,20 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
                                     co[0], co[1]);
         else
             at = block_append<256>(W.lvl + L + 1, nc);
+    } else if (W.hybrid) {
+        // the chain continues into level L + 1 (its first child), and a second child starts a side chain:
+        // both enter level L + 1's list; the side chain takes the next id of the side chains started at L + 1
+        // (after npaths and the side chains started at levels 1..L: read here, before the first store, as a
+        // load behind the stores would wait for all of them)
+        const int side = (child_depth > 0 && nchild > 1) ? 1 : 0, cont = (child_depth > 0 && nchild > 0) ? 1 : 0;
+        block_append2(W.lvl + L + 1, cont + side, W.lvl + LVL_SIDE + L + 1, side, at, side_at);
+        side_at += W.npaths;
+        for (int j = 1; j <= L; ++j) side_at += W.lvl[LVL_SIDE + j];
     }
     // ---- stores ----
     if (prim == NO_RAY) {
         if (in) store_node(W, i, f3(0, 0, 0), 0u);
+        if (CHAIN && W.hybrid && in) W.endl[r] = (uint8_t)L;
         return;
     }
     if (!hit) {  // miss: World.color returns bg_color (world.js:35-36)
@@ -708,6 +763,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         if (CHAIN) {
             store_node(W, i, bg, INFO_MISS);
             W.prim[r] = NO_RAY;
+            if (W.hybrid) W.endl[r] = (uint8_t)L;
         } else {
             if (parent == NO_PARENT) {  // write_result with the preloaded parent / path
                 float *dst = W.root + 3 * (size_t)path;
@@ -725,18 +781,35 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     if (nchild > 1 && unit_child(ch1)) out.info |= INFO_UNIT1;
     store_node(W, i, out.surf, out.info);
     if (out.info & INFO_LIT) {
-        if (CHAIN || !W.bucket) store_hand(W, q, out.h);
+        if (!W.bucket) store_hand(W, q, out.h);
         else if (hslot != ~0u) store_hand(W, hslot, out.h);
     }
     if (nchild > 0) store_child(W, i, 0, ch0);
     if (nchild > 1) store_child(W, i, 1, ch1);
     if (CHAIN) {  // the child ray (World.color(child, depth - 1)) takes over slot q
+        uint32_t *next = (L & 1) ? W.list0 : W.list1;  // level L + 1's list
         if (child_depth > 0 && nchild > 0) {
             W.ox[r] = out.h.pos.x; W.oy[r] = out.h.pos.y; W.oz[r] = out.h.pos.z;
             W.dx[r] = ch0.dir.x; W.dy[r] = ch0.dir.y; W.dz[r] = ch0.dir.z;
             W.addr[r] = mix32(out.h.addr, 1u);
+            if (W.hybrid) next[at] = r;
         } else {
             W.prim[r] = NO_RAY;  // no child, or children black without a cast (depth 0)
+            if (W.hybrid) W.endl[r] = (uint8_t)L;
+        }
+        if (W.hybrid && child_depth > 0 && nchild > 1) {  // the second child's side chain
+            const uint32_t c = side_at;  // npaths + side(< L + 1) + this chain's offset
+            if (c >= W.cap || at + 1 >= W.cap) {
+                W.lvl[LVL_FLAG] = 1u;  // out of chain slots: the host redoes the frame with more
+                return;
+            }
+            next[at + 1] = c;
+            W.ox[c] = out.h.pos.x; W.oy[c] = out.h.pos.y; W.oz[c] = out.h.pos.z;
+            W.dx[c] = ch1.dir.x; W.dy[c] = ch1.dir.y; W.dz[c] = ch1.dir.z;
+            W.addr[c] = mix32(out.h.addr, 2u);
+            W.key[c] = out.h.key;
+            W.parent[c] = i;
+            W.prim[c] = -1;
         }
         return;
     }
@@ -839,12 +912,8 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
 
 template <int PF, bool CHAIN, bool SERIAL>
 __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
+    const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+    const uint32_t count = R.count, base = R.base;
     const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     uint32_t q = e / G;  // G is a power of two
@@ -852,7 +921,7 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     bool in = q < count;
     const float4 *hp = W.hand + (in ? q : 0u);
     uint32_t mi = 0;  // the node's shadow-root mask (grid cell of its hit point)
-    if (!CHAIN && !SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
+    if (!SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
         in = q < as_const(W.bkt + (size_t)L * BKT_LEVEL)[3 * BKT_K];
         q = in ? f2u(hp[2 * W.hstride].w) : 0u;
         mi = f2u(hp[3 * W.hstride].w) & 0xFFu;
@@ -861,13 +930,14 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     // point in one grid cell -- the hand-off is bucketed by cell, so nearly every wave -- the world loop
     // visits only the roots a shadow segment from that cell can meet.
     uint64_t mask = ~0ull;
-    if (!CHAIN && !SERIAL && W.bucket && W.bucket_grid && S.grid_masked) {
+    if (!SERIAL && W.bucket && W.bucket_grid && S.grid_masked) {
         const uint64_t on = __ballot(in);
         if (on) {
             const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mi, __builtin_ctzll(on));
             if (!__ballot(in && mi != m0) && m0 <= (uint32_t)S.grid_cells) mask = as_const(S.grid_mask)[m0];
         }
     }
+    if (CHAIN && (SERIAL || !W.bucket) && in) q = chain_slot(W, L, q);  // hand-off in level order: the chain's slot
     const uint32_t i = base + (in ? q : 0u);
     const float4 nd = W.node[i];
     const bool lit = in && (f2u(nd.w) & INFO_LIT);
@@ -897,15 +967,17 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
 struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
     const WArgs &W;
     uint32_t base;
+    int L;  // chain schedule: >= 0, ray j is the level's j-th chain (chain_slot); tree: -1, ray base + j
+    __device__ __forceinline__ uint32_t ray(uint32_t j) const { return L >= 0 ? chain_slot(W, L, j) : base + j; }
     __device__ __forceinline__ bool load(uint32_t j, F3 &o, F3 &d) const {
-        const uint32_t i = base + j;
+        const uint32_t i = ray(j);
         if (W.prim[i] == NO_RAY) return false;
         o = f3(W.ox[i], W.oy[i], W.oz[i]);
         d = f3(W.dx[i], W.dy[i], W.dz[i]);
         return true;
     }
     __device__ __forceinline__ void store(uint32_t j, const Hit &h) const {
-        const uint32_t i = base + j;
+        const uint32_t i = ray(j);
         W.t[i] = h.t;
         W.prim[i] = h.prim;
         W.ctx[i] = h.ctx;
@@ -914,13 +986,9 @@ struct ExtendSrc {  // the level's rays (k_extend's inputs and outputs)
 
 template <int PF, bool CHAIN, bool FO>
 __global__ __launch_bounds__(256, JSRT_MARCH_OCC) void k_extend_q(DScene S, WArgs W, int L, double minD) {
-    uint32_t count = W.npaths, base = 0;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
-    ExtendSrc src{W, base};
+    const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+    const uint32_t count = R.count, base = CHAIN ? 0u : R.base;  // ray slots
+    ExtendSrc src{W, base, CHAIN ? L : -1};
     persistent_cast<PF, false, FO>(S, W.qctr + L, count, minD, DINF, true, src);
 }
 
@@ -943,17 +1011,13 @@ struct ShadowSrc {  // the light samples' shadow rays written by k_shadow_prep
 // colour and shadow ray of every light sample
 template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
+    const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+    const uint32_t count = R.count, base = R.base;
     const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     const uint32_t q = e / G, s = e % G;
     if (q >= count || s >= ns) return;
-    const float4 nd = W.node[base + q];
+    const float4 nd = W.node[base + (CHAIN ? chain_slot(W, L, q) : q)];
     if (!(f2u(nd.w) & INFO_LIT)) return;
     F3 P, delta;
     const F3 c = sample_unshadowed<PF>(S, W.hand + q, W.hstride, s, P, delta);
@@ -967,8 +1031,7 @@ __global__ __launch_bounds__(256) void k_shadow_prep(DScene S, WArgs W, int L) {
 
 template <int PF, bool CHAIN, bool FO>
 __global__ __launch_bounds__(256, JSRT_MARCH_OCC) void k_shadow_cast(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths;
-    if (!CHAIN) count = level_range(W, L).count;
+    const uint32_t count = CHAIN ? chain_level(W, L).count : level_range(W, L).count;
     ShadowSrc src{W};
     persistent_cast<PF, true, FO>(S, W.qctr + 32 + L, count * (uint32_t)W.group, 0.0001, 1, false, src);
 }
@@ -976,17 +1039,13 @@ __global__ __launch_bounds__(256, JSRT_MARCH_OCC) void k_shadow_cast(DScene S, W
 // colorFromLights' sums of k_shadow from the stored sample colours (shadowed: +0)
 template <bool CHAIN>
 __global__ __launch_bounds__(256) void k_shadow_sum(DScene S, WArgs W, int L) {
-    uint32_t count = W.npaths, base = (uint32_t)L * W.npaths;
-    if (!CHAIN) {
-        const LevelRange R = level_range(W, L);
-        count = R.count;
-        base = R.base;
-    }
+    const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
+    const uint32_t count = R.count, base = R.base;
     const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     const uint32_t q = e / G, s = e % G;
     const bool in = q < count;
-    const uint32_t i = base + (in ? q : 0u);
+    const uint32_t i = base + (in ? (CHAIN ? chain_slot(W, L, q) : q) : 0u);
     const float4 nd = W.node[i];
     const bool lit = in && (f2u(nd.w) & INFO_LIT);
     F3 c = f3(0, 0, 0);
@@ -1080,11 +1139,12 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
     // persistent casts for SDF scenes with a flat top level (W.sstride != 0 when enabled)
     const bool Q = (PF & PF_SDF) && W.sstride != 0;
     if (Q) (void)hipMemsetAsync(W.qctr, 0, 64 * sizeof(uint32_t), st);
-    if (!CHAIN && W.bucket) (void)hipMemsetAsync(W.bkt, 0, (size_t)MAX_TREE_DEPTH * BKT_LEVEL * sizeof(uint32_t), st);
+    if (W.bucket) (void)hipMemsetAsync(W.bkt, 0, (size_t)MAX_TREE_DEPTH * BKT_LEVEL * sizeof(uint32_t), st);
     timed(KT_GEN, [&] { hipLaunchKernelGGL(k_gen, dim3(grid(W.npaths)), dim3(256), 0, st, S, A, W); });
     std::vector<size_t> ubs;  // launch bound of each level's ray count
-    for (int L = 0; L < A.max_depth && (CHAIN || bound[L] > 0); ++L) {
-        const size_t ub = CHAIN ? (size_t)W.npaths : bound[L];
+    const bool learned = !CHAIN || W.hybrid;  // launch bounds from the host (learned level counts)
+    for (int L = 0; L < A.max_depth && (!learned || bound[L] > 0); ++L) {
+        const size_t ub = learned ? bound[L] : (size_t)W.npaths;
         ubs.push_back(ub);
         const int child_depth = A.max_depth - L - 1;
         timed(KT_EXTEND, [&] {
@@ -1097,7 +1157,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
             else
                 hipLaunchKernelGGL((k_extend<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L, L == 0 ? 0.0 : 0.0001);
         });
-        if (!CHAIN && W.bucket) hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(256), 0, st, W, L);
+        if (W.bucket) hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(256), 0, st, W, L);
         if (split && L > 0 && W.ns > 0) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the hand-off is free
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
@@ -1127,6 +1187,17 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         if (W.ns > 0 && split) (void)hipEventRecord(sync->shadow_done, ss);
     }
     if (split && W.ns > 0 && !ubs.empty()) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the lit colours
+    if (CHAIN && W.hybrid) {  // side chains deepest start first, then the paths; k_accum adds them in sample order
+        timed(KT_RESOLVE, [&] {
+            for (int s = (int)ubs.size() - 1; s >= 1; --s)  // (the chains started at s are live at s: <= ubs[s])
+                hipLaunchKernelGGL(k_resolve_side, dim3(grid_ub(ubs[s])), dim3(256), 0, st, A, W, s);
+            hipLaunchKernelGGL(k_resolve_paths, dim3(grid(W.npaths)), dim3(256), 0, st, A, W);
+        });
+        accum_wait();
+        timed(KT_ACCUM, [&] { hipLaunchKernelGGL(k_accum, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
+        accum_done();
+        return;
+    }
     if (CHAIN) {
         accum_wait();
         timed(KT_RESOLVE, [&] { hipLaunchKernelGGL(k_resolve, dim3(grid(W.npix)), dim3(256), 0, st, A, W); });
