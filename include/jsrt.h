@@ -93,6 +93,16 @@ int jsrt_render(jsrt_scene *scene, const jsrt_params *params, uint8_t *rgba8, fl
 int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
                        float *d_colors, void *hip_stream, jsrt_stats *stats);
 
+/* jsrt_render_device with progress (the multi-GPU tile path's preview cadence, renderers.js:103-112 /
+ * worker.js:30-32): progress(pass, completion) is called at most every params->timelimit_ms (0 = never;
+ * a tiny value = after every pass of params->samples_per_launch samples), from the calling thread, with
+ * the stream idle.  With the Incremental renderer, d_rgba8 (and d_colors) then hold the running mean of
+ * samples 0..pass of the owned columns -- the image the reference worker posts -- so a caller can gather
+ * the ranks' tiles inside the callback.  Returns when the frame is done (synchronous). */
+int jsrt_render_device_progress(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
+                                float *d_colors, void *hip_stream, jsrt_progress_fn progress, void *user,
+                                jsrt_stats *stats);
+
 /* World.cast(ray, min_dist, max_dist, intersect_transparent) (world.js:28-30) of n rays on the scene's
  * device: rays = n x 6 f32 host array (origin xyz with w = 1, direction xyz with w = 0, as
  * Camera.getRayForPixel and the materials make them).  out_dist (n f64): the closest hit's distance,

@@ -108,9 +108,8 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h, uint32_t v) {
     h ^= h >> 13;
     return h;
 }
-// pixkey = mix(mix(seed, pixel), sample), hoisted per sample
-__device__ __forceinline__ double keyed_uniform(uint32_t pixkey, uint32_t node, uint32_t call) {
-    const uint32_t h = mix32(mix32(pixkey, node), call);
+// the draw of hash h = mix(mix(pixkey, node), call)
+__device__ __forceinline__ double uniform_of(uint32_t h) {
     const uint32_t hi = mix32(h, 0xA5A5A5A5u) >> 5;  // 27 bits
     const uint32_t lo = mix32(h, 0x5A5A5A5Au) >> 6;  // 26 bits
     // (hi * 2^26 + lo) * 2^-53 with every step exact in f64 (hi * 2^-27 and lo * 2^-53 are exact, their sum
@@ -118,9 +117,19 @@ __device__ __forceinline__ double keyed_uniform(uint32_t pixkey, uint32_t node, 
     // multiply and the u64 -> f64 conversion sequence
     return fma((double)hi, 1.0 / 134217728.0, (double)lo * (1.0 / 9007199254740992.0));
 }
+// pixkey = mix(mix(seed, pixel), sample), hoisted per sample
+__device__ __forceinline__ double keyed_uniform(uint32_t pixkey, uint32_t node, uint32_t call) {
+    return uniform_of(mix32(mix32(pixkey, node), call));
+}
 struct Rng {
     uint32_t key, node, calls;
     __device__ __forceinline__ double next() { return keyed_uniform(key, node, calls++); }
+};
+// the same stream from the frame hash h0 = mix(pixkey, node), computed once per ray-tree node (the shadow
+// hand-off carries it in place of the key and the node address)
+struct RngH {
+    uint32_t h0, calls;
+    __device__ __forceinline__ double next() { return uniform_of(mix32(h0, calls++)); }
 };
 
 // --------------------------------------------------------------------------------------------
@@ -1094,23 +1103,30 @@ struct ShadeData {    // material_data after getBaseFactors (materials.js:210-23
 };
 
 // PhongMaterial.colorFromLightSample / FresnelPhongMaterial.colorFromLightSample
-// L = the sample direction normalised (light_sample computes it once for both uses)
-__device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, F3 L, F3 lcol) {
+// L = the sample direction normalised (light_sample computes it once for both uses).
+// spec_zero: the specular colour is (+0, +0, +0), the smoothness in [0, 1e5] and R finite (the loader's
+// MATF_SPEC_ZERO and k_shade's check).  Then every specular power the reference would compute is finite
+// (its base is a dot of two unit f32 vectors, at most 1 + 3e-7), spec.times(specular) is +0 and the
+// specular term is lcol * +0 whatever its value: the power is skipped.  Its one other effect, a NaN from a
+// NaN L, is kept: for Phong, L.dot(R) is NaN exactly when L.dot(N) is (R and N finite), and a NaN L.dot(N)
+// already makes the diffuse term NaN; the Fresnel terms are guarded by ldotn comparisons a NaN fails.
+__device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, F3 L, F3 lcol, bool spec_zero = false) {
     double diffuse, specular;
     if (mkind == JSRT_MAT_PHONG) {  // materials.js:261-269
-        diffuse = js_max(dot3(L, d.N), 0);
-        specular = js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
+        const double ldotn = dot3(L, d.N);
+        diffuse = js_max(ldotn, 0);
+        specular = spec_zero ? (is_nan(ldotn) ? ldotn : 0.0) : js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
     } else {  // materials.js:340-356
         const double ldotn = dot3(L, d.N);
         diffuse = 0;
         specular = 0;
         if (d.kr > 0 && ldotn >= 0) {
             diffuse += d.kr * ldotn;
-            specular += d.kr * js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
+            if (!spec_zero) specular += d.kr * js_pow(js_max(dot3(L, d.R), 0), d.smoothness);
         }
         if (d.kr < 1 && ldotn <= 0) {
             diffuse += (1 - d.kr) * -ldotn;
-            specular += (1 - d.kr) * js_pow(js_max(dot3(L, d.refr), 0), d.smoothness);
+            if (!spec_zero) specular += (1 - d.kr) * js_pow(js_max(dot3(L, d.refr), 0), d.smoothness);
         }
     }
     return add(mul(lcol, scale(d.diff, diffuse)), mul(lcol, scale(d.spec, specular)));
@@ -1119,8 +1135,8 @@ __device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, 
 // One sample of lights.js sampleIterator for `Lt` seen from world point P: the direction (delta, NOT
 // normalised: the shadow ray's t in (1e-4, 1) spans the segment) and the sample colour.
 // LT: DLight in any address space (a wave-uniform record is read through the constant one: scalar loads)
-template <class LT>
-__device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P, Rng &rng, F3 &delta, F3 &L,
+template <class LT, class RNG>
+__device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P, RNG &rng, F3 &delta, F3 &L,
                                              F3 &lcol) {
     if (Lt.kind == JSRT_LIGHT_POINT) {  // SimplePointLight.sampleIterator (lights.js:45-53)
         delta = sub(f3(Lt.pos[0], Lt.pos[1], Lt.pos[2]), P);

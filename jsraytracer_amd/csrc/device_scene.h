@@ -112,7 +112,10 @@ struct DCamera {         // cameras.js:18-53
     int32_t kind, pad[3];
 };
 
-enum { MATF_UV = 1 };  // material colours depend on (u, v): a checkerboard in some chain
+// material flags: MATF_UV colours depend on (u, v) (a checkerboard in some chain); MATF_DIFF_CONST /
+// MATF_SPEC_CONST the diffuse / specular chain is a constant (mc_const); MATF_SPEC_ZERO the specular colour
+// is the constant (+0, +0, +0) and the smoothness in [0, 1e5] (render_levels.h: no specular power)
+enum { MATF_UV = 1, MATF_DIFF_CONST = 2, MATF_SPEC_CONST = 4, MATF_SPEC_ZERO = 8 };
 
 struct DScene {
     const DPrim *prims;

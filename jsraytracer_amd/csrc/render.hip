@@ -201,9 +201,9 @@ __device__ __forceinline__ F3 resolve_chain(const RenderArgs &A, const WArgs &W,
 __global__ __launch_bounds__(256) void k_resolve_side(RenderArgs A, WArgs W, int s) {
     if (W.lvl[LVL_FLAG]) return;
     uint32_t lo = W.npaths;
-    for (int j = 1; j < s; ++j) lo += W.lvl[LVL_SIDE + j];
+    for (int j = 1; j < s; ++j) lo += W.lvl[2 * j + 1];
     const uint32_t c = lo + blockIdx.x * 256 + threadIdx.x;
-    if (c >= lo + W.lvl[LVL_SIDE + s]) return;
+    if (c >= lo + W.lvl[2 * s + 1]) return;
     const F3 v = resolve_chain(A, W, c, s);
     W.slot[W.parent[c]] = make_float4(v.x, v.y, v.z, 0.0f);
 }
@@ -279,7 +279,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree) bytes += need(2 * nodes, 16);                          // slot
     if (hybrid) bytes += need(nodes, 16);                            // slot (second children)
     if (tree || hybrid) bytes += need(3 * paths, 4);                 // root
-    bytes += need(HAND_PLANES * hands, 16) + need(64, 4);            // hand-off + level counts
+    bytes += need(HAND_PLANES * hands, 16) + need(hands, 4) + need(64, 4);  // hand-off + nodes + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
     if (tree || hybrid)  // buckets
         bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);
@@ -312,6 +312,7 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (hybrid) w.slot = carve<float4>(p, nodes);
     if (tree || hybrid) w.root = carve<float>(p, 3 * paths);
     w.hand = carve<float4>(p, HAND_PLANES * hands);
+    w.hnode = carve<uint32_t>(p, hands);
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
@@ -352,7 +353,7 @@ int schedule_of(const DScene &S) {
 constexpr size_t HYBRID_POOL_FACTOR = 2;  // initial hybrid side-chain slots: paths x factor / 4
 
 size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth) {
-    const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = HAND_PLANES * 16;
+    const size_t ray = 8 * 4 + 8 + 2 * 4, node = 16 + 4 * 16, hand = HAND_PLANES * 16 + 4;
     const bool persist = (S.profile & PF_SDF) && S.all_roots_prims;
     size_t group = 1;
     while ((int)group < ns && ns <= 64) group *= 2;
@@ -647,7 +648,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             W2.ox = t.ox; W2.oy = t.oy; W2.oz = t.oz; W2.dx = t.dx; W2.dy = t.dy; W2.dz = t.dz;
             W2.addr = t.addr; W2.key = t.key; W2.path = t.path; W2.parent = t.parent; W2.t = t.t;
             W2.prim = t.prim; W2.ctx = t.ctx; W2.node = t.node; W2.child = t.child; W2.slot = t.slot;
-            W2.hand = t.hand; W2.root = t.root; W2.lvl = t.lvl; W2.qctr = t.qctr; W2.sray = t.sray;
+            W2.hand = t.hand; W2.hnode = t.hnode; W2.root = t.root; W2.lvl = t.lvl; W2.qctr = t.qctr; W2.sray = t.sray;
             W2.scol = t.scol; W2.bkt = t.bkt; W2.bbase = t.bbase; W2.brank = t.brank;
             W2.list0 = t.list0; W2.list1 = t.list1; W2.endl = t.endl;
         }
@@ -742,7 +743,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) {
                         if (wf.frac.size() < (size_t)A.max_depth) wf.frac.assign(A.max_depth, 0.0);
                         for (int L = 0; L < A.max_depth; ++L)
-                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[L] / (double)Wb.npaths);
+                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[hybrid ? 2 * L : L] / (double)Wb.npaths);
                     }
                 }
             }

@@ -13,7 +13,7 @@ namespace jsrt {
 constexpr int MAX_TREE_DEPTH = 16;  // maxRecursionDepth supported (levels of the breadth-first schedule)
 constexpr int LVL_FLAG = 63;        // WArgs::lvl word set when a batch outgrew its pool (frame redone)
 constexpr int LVL_UNDER = 62;       // WArgs::lvl word set when a level outgrew its launch bound
-constexpr int LVL_SIDE = 16;        // hybrid chain: WArgs::lvl[LVL_SIDE + s] = side chains started at level s
+static_assert(2 * MAX_TREE_DEPTH + 2 <= LVL_UNDER, "hybrid chain count pairs lvl[2L, 2L + 1] below the flags");
 constexpr int BKT_N = 64;           // buckets of the shadow hand-off (hit primitive >> shift)
 constexpr int BKT_S = 16;           // slices per bucket (block index % BKT_S): spreads the counters' atomics
 constexpr int BKT_K = BKT_N * BKT_S;  // counters per level, key = bucket * BKT_S + slice
@@ -45,8 +45,9 @@ constexpr int INFO_NCHILD_SHIFT = 2;
 //         records are level-major [L * cap + q]; the child ray replaces its parent's ray.
 //         hybrid chain (branching materials, W.hybrid): the same, and a node's second child starts a
 //         side chain in a slot appended after the paths (the chains started at level s have the ids
-//         npaths + [side(< s), side(<= s)), side counts lvl[LVL_SIDE + s]).  Level L > 0 visits only its
-//         live chains, listed by k_shade(L - 1) (list[L & 1], lvl[L] entries); a chain's last level is
+//         npaths + [side(< s), side(<= s))).  Level L > 0 visits only its live chains, listed by
+//         k_shade(L - 1) (list[L & 1]).  Counts: the 64-bit word lvl[2L, 2L + 1] = {live chains of level L,
+//         side chains started at L}, appended with one 64-bit atomic per block.  A chain's last level is
 //         endl[slot].  A side chain's colour is resolved bottom-up before its parent's and left in
 //         slot[parent node] (k_resolve_side).
 //   tree  (branching materials): rays and nodes share pool slots; level L occupies
@@ -67,6 +68,7 @@ struct WArgs {
     float4 *child;     // [(2 * j + part) * nstride + i]: part 0 {col.xyz, w.x}, part 1 {w.y, w.z, k (f64)}
     float4 *slot;      // tree: [j * nstride + i] the child's colour; hybrid chain: [i] the second child's
     float4 *hand;      // [k * hstride + h], k < 6: shadow hand-off of a lit node (h: path / level index, render_levels.h store_hand)
+    uint32_t *hnode;   // [h]: the node (level index / chain slot) of bucketed hand-off slot h
     float *root;       // tree: [3 * path] root colours
     uint32_t *lvl;     // tree: [L] ray count of level L; [LVL_FLAG] overflow flag
     uint32_t *list0, *list1;  // hybrid chain: the live chain slots of odd (list1) / even (list0) levels > 0

@@ -79,9 +79,11 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, int n) {
     return s_off[NW] + s_off[wid] + pre;
 }
 
-// Two block-aggregated appends at once (one atomic per block on each counter): n0 (0..2) entries on c0 and
-// n1 (0..1) on c1.  Every thread of the block must call it; o0 / o1 = this thread's first offsets.
-__device__ __forceinline__ void block_append2(uint32_t *c0, int n0, uint32_t *c1, int n1, uint32_t &o0, uint32_t &o1) {
+// Two block-aggregated appends at once, one 64-bit atomic per block on a counter pair (ctr[0], ctr[1]):
+// n0 (0..2) entries on the low word and n1 (0..1) on the high one (two atomics on one L2 line serialise:
+// measured, k_shade 2.6 -> 7.9 ms per cornell launch).  Every thread of the block must call it; o0 / o1 =
+// this thread's first offsets.
+__device__ __forceinline__ void block_append2(uint32_t *ctr, int n0, int n1, uint32_t &o0, uint32_t &o1) {
     constexpr int NW = 256 / 64;
     __shared__ uint32_t s0[NW + 1], s1[NW + 1];
     const uint64_t a1 = __ballot(n0 >= 1), a2 = __ballot(n0 >= 2), b1 = __ballot(n1 >= 1);
@@ -102,8 +104,10 @@ __device__ __forceinline__ void block_append2(uint32_t *c0, int n0, uint32_t *c1
             x0 += c;
             x1 += d;
         }
-        s0[NW] = x0 ? atomicAdd(c0, x0) : 0u;
-        s1[NW] = x1 ? atomicAdd(c1, x1) : 0u;
+        const unsigned long long old =
+            (x0 | x1) ? atomicAdd(reinterpret_cast<unsigned long long *>(ctr), ((unsigned long long)x1 << 32) | x0) : 0ull;
+        s0[NW] = (uint32_t)old;
+        s1[NW] = (uint32_t)(old >> 32);
     }
     __syncthreads();
     o0 = s0[NW] + s0[wid] + p0;
@@ -211,13 +215,21 @@ __device__ __forceinline__ LevelRange chain_level(const WArgs &W, int L) {
     const uint32_t base = (uint32_t)L * W.cap;
     if (!W.hybrid) return LevelRange{base, W.npaths};
     if (W.lvl[LVL_FLAG]) return LevelRange{base, 0u};
-    return LevelRange{base, W.lvl[L]};
+    return LevelRange{base, W.lvl[2 * L]};  // (the low word of level L's count pair)
 }
 // the chain slot of level L's t-th visited chain
 __device__ __forceinline__ uint32_t chain_slot(const WArgs &W, int L, uint32_t t) {
     if (!W.hybrid || L == 0) return t;
     return ((L & 1) ? W.list1 : W.list0)[t];
 }
+
+// shadow hand-off plane flags (store_hand)
+constexpr uint32_t HAND_KR = 0x80000000u;    // planes 3 .w and 5: kr != 1 (and refr)
+constexpr uint32_t HAND_DIFF = 0x40000000u;  // plane 2: diff is not the material's constant
+constexpr uint32_t HAND_R = 0x20000000u;     // plane 3: the specular term needs R
+constexpr uint32_t HAND_SPEC = 0x10000000u;  // plane 4: spec is not the material's constant
+constexpr uint32_t HAND_MAT = 0x0FFFFF00u;   // mat << 8
+constexpr int HAND_PLANES = 6;
 
 // The material data k_shade hands to k_shadow for one lit node (after getBaseFactors), plus the
 // node's RNG frame (its light-sample draws come first, materials.js:244-257).
@@ -226,8 +238,9 @@ struct Handoff {
     double kr;
     int32_t mkind, mat;
     uint32_t addr, key;
-    uint32_t node;  // the node's level index (bucketed hand-off: where k_shadow writes its colour)
-    uint32_t mask;  // shadow-root mask index (DScene::grid_mask) of the node's hit point
+    uint32_t node;   // the node's level index / chain slot (bucketed hand-off: where k_shadow writes its colour)
+    uint32_t mask;   // shadow-root mask index (DScene::grid_mask) of the node's hit point
+    uint32_t flags;  // HAND_*: the optional planes this node stores
 };
 struct NodeOut {
     F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
@@ -491,6 +504,17 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         out.h.kr = sd.kr;
         out.h.mkind = mkind;
         out.h.mat = P.material;
+        // the planes k_shadow needs beyond P, N (store_hand): a colour the material does not hold as a
+        // constant, R unless the specular term is provably +0 (light_sample_color spec_zero), kr / refr
+        // where kr != 1 (colorFromLightSample never reads refr with kr == 1, materials.js:349-354)
+        const int32_t mf = S.mat_flags[P.material];
+        uint32_t fl = 0;
+        if (!(mf & MATF_DIFF_CONST) || sf.has_bc) fl |= HAND_DIFF;  // diff = basecolor x the diffuse chain
+        if (!(mf & MATF_SPEC_CONST)) fl |= HAND_SPEC;
+        if (mkind != JSRT_MAT_PHONG && sd.kr != 1.0) fl |= HAND_KR | HAND_R;
+        if (!(mf & MATF_SPEC_ZERO) || !(__builtin_isfinite(sd.R.x) && __builtin_isfinite(sd.R.y) && __builtin_isfinite(sd.R.z)))
+            fl |= HAND_R;
+        out.h.flags = fl;
         rng.calls = (uint32_t)S.light_draws;
     }
     int n = 0;
@@ -549,25 +573,25 @@ __device__ __forceinline__ F3 add_child(const WArgs &W, uint32_t i, uint32_t j, 
     const double k = __hiloint2double((int)f2u(b.w), (int)f2u(b.z));
     return add(c, scale(mul(mul(v, f3(a.x, a.y, a.z)), f3(a.w, b.x, b.y)), k));
 }
-// Hand-off record: planes of one float4 per lit node (plane stride hstride), 80 B, plus a sixth plane
-// only where kr != 1 (FresnelPhong / path tracing with a finite ratio):
-//   0 {P, addr}  1 {N, key}  2 {R, node}  3 {diff, mat << 8 | mask | HAND_KR}  4 {spec, hi(kr)}
-//   5 {refr, lo(kr)}
-// The material's kind and smoothness are read from its record (S.mat) by the sample.  With kr == 1
-// colorFromLightSample never reads refr (materials.js:349-354), and a Phong material never reads kr.
-constexpr uint32_t HAND_KR = 0x80000000u;  // plane 5 holds refr and lo(kr); kr != 1
-constexpr int HAND_PLANES = 6;
+// Hand-off record of a lit node: float4 planes (plane stride hstride), two always and the rest as the
+// node's material needs them (Handoff::flags, in the tag), plus the node index where the hand-off is
+// bucketed (hnode[h], k_shadow's write-back address):
+//   0 {P, h0 = mix(key, addr)}  1 {N, tag = mat << 8 | mask | HAND_*}
+//   2 {diff} HAND_DIFF  3 {R, hi(kr)} HAND_R  4 {spec} HAND_SPEC  5 {refr, lo(kr)} HAND_KR
+// A colour without its plane is the material's constant (S.mc_const); the material's kind and smoothness
+// come from its record (S.mat).  cornell's walls need 36 B (80 B until round 4), its floor 68 B.
 __device__ __forceinline__ void store_hand(const WArgs &W, uint32_t h, const Handoff &o) {
     float4 *p = W.hand + h;
     const size_t hs = W.hstride;
-    const bool kr_plane = o.mkind != JSRT_MAT_PHONG && o.kr != 1.0;
-    const uint32_t tag = ((uint32_t)o.mat << 8) | (o.mask & 0xFFu) | (kr_plane ? HAND_KR : 0u);
-    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f(o.addr));
-    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f(o.key));
-    p[2 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f(o.node));
-    p[3 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, u2f(tag));
-    p[4 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, u2f((uint32_t)__double2hiint(o.kr)));
-    if (kr_plane) p[5 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f((uint32_t)__double2loint(o.kr)));
+    const uint32_t fl = o.flags;
+    const uint32_t tag = ((uint32_t)o.mat << 8) | (o.mask & 0xFFu) | fl;
+    p[0] = make_float4(o.pos.x, o.pos.y, o.pos.z, u2f(mix32(o.key, o.addr)));
+    p[hs] = make_float4(o.N.x, o.N.y, o.N.z, u2f(tag));
+    if (fl & HAND_DIFF) p[2 * hs] = make_float4(o.diff.x, o.diff.y, o.diff.z, 0.0f);
+    if (fl & HAND_R) p[3 * hs] = make_float4(o.R.x, o.R.y, o.R.z, u2f((uint32_t)__double2hiint(o.kr)));
+    if (fl & HAND_SPEC) p[4 * hs] = make_float4(o.spec.x, o.spec.y, o.spec.z, 0.0f);
+    if (fl & HAND_KR) p[5 * hs] = make_float4(o.refr.x, o.refr.y, o.refr.z, u2f((uint32_t)__double2loint(o.kr)));
+    if (W.bucket) W.hnode[h] = o.node;
 }
 
 // per pixel, the renderer's f32 accumulation of one sample (renderers.js:93-97, 52-61)
@@ -748,9 +772,9 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         // (after npaths and the side chains started at levels 1..L: read here, before the first store, as a
         // load behind the stores would wait for all of them)
         const int side = (child_depth > 0 && nchild > 1) ? 1 : 0, cont = (child_depth > 0 && nchild > 0) ? 1 : 0;
-        block_append2(W.lvl + L + 1, cont + side, W.lvl + LVL_SIDE + L + 1, side, at, side_at);
+        block_append2(W.lvl + 2 * (L + 1), cont + side, side, at, side_at);
         side_at += W.npaths;
-        for (int j = 1; j <= L; ++j) side_at += W.lvl[LVL_SIDE + j];
+        for (int j = 1; j <= L; ++j) side_at += as_const(W.lvl)[2 * j + 1];  // (scalar loads: stable words)
     }
     // ---- stores ----
     if (prim == NO_RAY) {
@@ -846,33 +870,40 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
 // One light sample of a lit node without its shadow cast: the light sample (lights.js), its
 // unshadowed colour (colorFromLightSample) and the shadow ray (origin P = the hit point, direction
 // delta, accepted distances (1e-4, 1), materials.js:250-252).
+__device__ __forceinline__ F3 mc_const3(const DScene &S, int m) {  // a constant colour chain's value
+    const float4 c = *reinterpret_cast<const float4 *>(S.mc_const + 4 * m);
+    return f3(c.x, c.y, c.z);
+}
 template <int PF>
 __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
     const float4 h0 = hp[0], h1 = hp[hs];
     P = f3(h0.x, h0.y, h0.z);
-    Rng rng{f2u(h1.w), f2u(h0.w), (uint32_t)S.sample_call[s]};
+    RngH rng{f2u(h0.w), (uint32_t)S.sample_call[s]};
     F3 L, lcol;
     if (S.n_lights == 1)  // (kernel argument: uniform) the light record through scalar loads
         light_sample(S, as_const(S.lights)[0], P, rng, delta, L, lcol);
     else
         light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
-    const float4 h2 = hp[2 * hs], h3 = hp[3 * hs], h4 = hp[4 * hs];
-    const uint32_t tag = f2u(h3.w);
-    const jsrt_rec_material &M = S.mat[(tag & ~HAND_KR) >> 8];
+    const uint32_t tag = f2u(h1.w);
+    const jsrt_rec_material &M = S.mat[(tag & HAND_MAT) >> 8];
     ShadeData sd;
     sd.N = f3(h1.x, h1.y, h1.z);
-    sd.R = f3(h2.x, h2.y, h2.z);
-    sd.diff = f3(h3.x, h3.y, h3.z);
-    sd.spec = f3(h4.x, h4.y, h4.z);
+    sd.diff = (tag & HAND_DIFF) ? f3(hp[2 * hs].x, hp[2 * hs].y, hp[2 * hs].z) : mc_const3(S, M.diffuse);
+    sd.spec = (tag & HAND_SPEC) ? f3(hp[4 * hs].x, hp[4 * hs].y, hp[4 * hs].z) : mc_const3(S, M.specular);
+    sd.R = f3(0, 0, 0);
     sd.refr = f3(0, 0, 0);
     sd.kr = 1.0;
-    if (tag & HAND_KR) {
-        const float4 h5 = hp[5 * hs];
-        sd.refr = f3(h5.x, h5.y, h5.z);
-        sd.kr = __hiloint2double((int)f2u(h4.w), (int)f2u(h5.w));
+    if (tag & HAND_R) {
+        const float4 h3 = hp[3 * hs];
+        sd.R = f3(h3.x, h3.y, h3.z);
+        if (tag & HAND_KR) {
+            const float4 h5 = hp[5 * hs];
+            sd.refr = f3(h5.x, h5.y, h5.z);
+            sd.kr = __hiloint2double((int)f2u(h3.w), (int)f2u(h5.w));
+        }
     }
     sd.smoothness = M.smoothness;
-    return light_sample_color((int)M.kind, sd, L, lcol);
+    return light_sample_color((int)M.kind, sd, L, lcol, !(tag & HAND_R));
 }
 
 __device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
@@ -923,8 +954,9 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     uint32_t mi = 0;  // the node's shadow-root mask (grid cell of its hit point)
     if (!SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
         in = q < as_const(W.bkt + (size_t)L * BKT_LEVEL)[3 * BKT_K];
-        q = in ? f2u(hp[2 * W.hstride].w) : 0u;
-        mi = f2u(hp[3 * W.hstride].w) & 0xFFu;
+        const uint32_t h = in ? q : 0u;
+        q = W.hnode[h];
+        mi = f2u(hp[W.hstride].w) & 0xFFu;
     }
     // Shadow-root mask of the wave (scene_load.cpp shadow_grid): when every node of the wave has its hit
     // point in one grid cell -- the hand-off is bucketed by cell, so nearly every wave -- the world loop

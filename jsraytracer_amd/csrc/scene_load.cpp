@@ -851,9 +851,9 @@ struct Loader {
         S.cam.sensor = C.sensor_size;
         S.cam.kind = (int32_t)C.kind;
 
-        // the shadow hand-off packs the material index into 23 bits beside the kr flag (render_levels.h
-        // store_hand: mat << 8 | mask | HAND_KR)
-        if (B.n_mat >= (1u << 23)) fail("more than 2^23 materials");
+        // the shadow hand-off packs the material index into 20 bits beside the grid mask and its plane flags
+        // (render_levels.h store_hand: mat << 8 | mask | HAND_*)
+        if (B.n_mat >= (1u << 20)) fail("more than 2^20 materials");
         for (uint32_t i = 0; i < B.n_mat; ++i) {
             const jsrt_rec_material &M = B.mat[i];
             if (M.kind < JSRT_MAT_PHONG || M.kind > JSRT_MAT_TRANSPARENT) fail("unsupported material kind");
@@ -873,6 +873,20 @@ struct Loader {
         }
         for (uint32_t i = 0; i < B.n_mc; ++i) S.mc.push_back(B.mc[i]);
         mc_constants();
+        // constant diffuse / specular colours (k_shadow reads them from mc_const, not the hand-off)
+        for (size_t i = 0; i < S.mat.size(); ++i) {
+            const jsrt_rec_material &M = S.mat[i];
+            if (M.kind == JSRT_MAT_SOLID || M.kind == JSRT_MAT_TRANSPARENT) continue;
+            const float *d = &S.mc_const[4 * (size_t)M.diffuse], *sp = &S.mc_const[4 * (size_t)M.specular];
+            if (d[3] != 0.0f) S.mat_flags[i] |= MATF_DIFF_CONST;
+            if (sp[3] != 0.0f) {
+                S.mat_flags[i] |= MATF_SPEC_CONST;
+                uint32_t b[3];
+                memcpy(b, sp, sizeof b);
+                if (b[0] == 0u && b[1] == 0u && b[2] == 0u && M.smoothness >= 0.0 && M.smoothness <= 1e5)
+                    S.mat_flags[i] |= MATF_SPEC_ZERO;
+            }
+        }
 
         const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
         for (int k = 0; k < 16; ++k) S.ctx.push_back(I[k]);  // ctx 0: World.color's Mat4.identity()

@@ -125,15 +125,33 @@ class Scene:
         check(rc, "jsrt_render")
         return rgba, colors, st.as_dict()
 
-    def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, stats=True, **kw):
+    def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, stats=True, progress=None,
+                      **kw):
         """Render owned columns into device buffers (see jsrt.h jsrt_render_device).  stats=False
-        records no per-launch HIP events (and returns None)."""
+        records no per-launch HIP events (and returns None).  progress(pass, completion): called at the
+        timelimit_ms cadence with the device buffers holding the running mean of the passes done (Incremental;
+        jsrt_render_device_progress) -- synchronous, the stream idle in the callback."""
         L = _native.lib()
         p = self.params(device=self.device, **kw)
         st = Stats() if stats else None
-        rc = L.jsrt_render_device(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
-                                  ctypes.byref(st) if stats else None)
-        check(rc, "jsrt_render_device")
+        if progress is None:
+            rc = L.jsrt_render_device(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
+                                      ctypes.byref(st) if stats else None)
+            check(rc, "jsrt_render_device")
+            return st.as_dict() if stats else None
+        err = []
+
+        def tramp(pass_, completion, _user):
+            try:
+                progress(int(pass_), float(completion))
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the frame
+                err.append(e)
+        cb = _native.PROGRESS_FN(tramp)
+        rc = L.jsrt_render_device_progress(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
+                                           cb, None, ctypes.byref(st) if stats else None)
+        if err:
+            raise err[0]
+        check(rc, "jsrt_render_device_progress")
         return st.as_dict() if stats else None
 
     def header(self):

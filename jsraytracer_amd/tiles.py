@@ -70,3 +70,41 @@ class FrameGather:
     def to_rgba8(image):
         """[H, W] int32 packed RGBA8 (little-endian R first) -> [H, W, 4] uint8 numpy."""
         return image.cpu().numpy().view(np.uint8).reshape(image.shape[0], image.shape[1], 4)
+
+
+def render_progressive(scene, fg, dev_tile, on_preview, timelimit_ms=0.0, host_tiles=False, **kw):
+    """Progressive multi-rank render of one frame: the reference's workers post their partial image at every
+    `timelimit` tick (src/worker.js:30-32, src/renderers.js:103-112) and the main thread overlays them
+    (src/raytrace_launcher.js:92-97).  Every rank renders its tile with jsrt_render_device_progress, one
+    sample per pixel per pass, so its device tile holds the running mean of passes 0..p at each callback.
+    Rank 0's clock decides whether a preview is due (one broadcast per pass keeps the ranks' collectives in
+    step); when it is, the ranks' tiles are gathered (FrameGather, RCCL over xGMI or gloo) and rank 0 gets
+    on_preview(pass, image [H, W] int32 RGBA8).  The frame's final tile is left in dev_tile.
+
+    kw: jsrt_render_device parameters (width, height, spp, max_depth, kind, seed, x_offset, x_delt)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    last = [time.perf_counter()]
+    flag = torch.zeros(1, dtype=torch.int32, device="cpu" if host_tiles or fg.world == 1 else dev_tile.device)
+
+    def cb(p, _completion):
+        if fg.rank == 0:
+            now = time.perf_counter()
+            due = (now - last[0]) * 1e3 >= timelimit_ms
+            if due:
+                last[0] = now
+            flag.fill_(1 if due else 0)
+        if fg.world > 1:
+            dist.broadcast(flag, src=0)
+        if not int(flag.item()):
+            return
+        fg.local.copy_(dev_tile.view(-1)[:fg.local.numel()].to(fg.local.device))
+        img = fg.gather()
+        if fg.rank == 0:
+            on_preview(p, img)
+
+    # every pass calls back on every rank (a 1e-9 ms library cadence); the preview cadence is rank 0's
+    scene.render_device(dev_tile.data_ptr(), progress=cb, timelimit_ms=1e-9, samples_per_launch=1, stats=False,
+                        col_block=fg.cb, **kw)

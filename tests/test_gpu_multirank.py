@@ -60,3 +60,53 @@ def test_gpu_rank_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
     full, _, _ = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0).render(W, H, SPP, DEPTH, 1, 1,
                                                                                      want_colors=False)
     assert np.array_equal(comp, full)
+
+
+PSPP = 4  # progressive frame: passes 0..PSPP-2 call back, the last pass is the final frame
+
+
+def _rank_progressive(rank, world, port, cb, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import jsraytracer_amd as jr
+    from jsraytracer_amd.tiles import FrameGather, render_progressive
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    fg = FrameGather(W, H, rank, world, cb)  # host tiles: gloo gathers CPU tensors
+    dev = torch.zeros(fg.maxcols * H, dtype=torch.int32, device="cuda:0")
+
+    def keep(p, img):
+        np.save(os.path.join(outdir, f"pass{p}.npy"), FrameGather.to_rgba8(img))
+
+    render_progressive(sc, fg, dev, keep, timelimit_ms=0.0, host_tiles=True, width=W, height=H, spp=PSPP,
+                       max_depth=DEPTH, kind=1, seed=1, x_offset=rank, x_delt=world)
+    fg.local.copy_(dev.cpu())
+    img = fg.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "final.npy"), FrameGather.to_rgba8(img))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 16), (3, 8)])
+def test_gpu_progressive_previews_gather_to_running_mean(tmp_path, world, cb):
+    """The multi-GPU tile path with progress (jsrt_render_device_progress + tiles.render_progressive): at
+    every pass p the ranks' tiles hold the running mean of samples 0..p (renderers.js:93-112), rank 0
+    gathers them, and the composite equals the single-rank frame of spp = p + 1 bit for bit (keyed RNG:
+    sample k of a pixel does not depend on spp); the final gather equals the full frame."""
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    mp.start_processes(_rank_progressive, args=(world, _free_port(), cb, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    for p in range(PSPP - 1):
+        got = np.load(os.path.join(tmp_path, f"pass{p}.npy"))
+        ref, _, _ = sc.render(W, H, p + 1, DEPTH, 1, 1, want_colors=False)
+        assert np.array_equal(got, ref), f"pass {p}: {int((got != ref).any(-1).sum())} pixels differ"
+    full, _, _ = sc.render(W, H, PSPP, DEPTH, 1, 1, want_colors=False)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "final.npy")), full)

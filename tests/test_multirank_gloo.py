@@ -75,3 +75,69 @@ def test_owned_columns_cover_the_frame_once():
                     assert len(owned_px(W, r, world, cb)) == owned_columns(W, r, world, cb)
                 slot = column_permutation(W, world, cb)
                 assert len(set(slot.tolist())) == W and slot.max() < world * max_owned(W, world, cb)
+
+
+class _OracleTileScene:
+    """Stands in for jr.Scene on the CPU: render_device fills `tile` pass by pass with the oracle's running
+    mean of the rank's owned columns (the oracle's spp = p + 1 render, which the keyed RNG makes the
+    Incremental renderer's image after pass p) and calls progress after every pass but the last, as
+    jsrt_render_device_progress does."""
+
+    def __init__(self, blob, tile, W, H, cols):
+        self.blob, self.tile, self.W, self.H, self.cols = blob, tile, W, H, cols
+
+    def render_device(self, ptr, progress=None, timelimit_ms=0.0, samples_per_launch=0, stats=False, col_block=1,
+                      width=0, height=0, spp=1, max_depth=4, kind=1, seed=1, x_offset=0, x_delt=1):
+        import torch
+
+        from oracle import pyoracle
+        assert samples_per_launch == 1 and timelimit_ms > 0 and progress is not None
+        for p in range(spp):
+            t = np.zeros((len(self.cols), self.H), np.uint32)
+            for c, px in enumerate(self.cols):
+                _, rgba, _ = pyoracle.render(self.blob, self.W, self.H, p + 1, max_depth, kind, seed, int(px), self.W,
+                                             threads=1)
+                t[c] = rgba[:, px].view(np.uint32).reshape(self.H)
+            self.tile.zero_()
+            self.tile[:t.size].copy_(torch.from_numpy(t.view(np.int32).reshape(-1)))
+            if p < spp - 1:
+                progress(p, (p + 1) / spp)
+
+
+def _progressive_worker(rank, world, port, W, H, cb, spp, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from jsraytracer_amd.tiles import FrameGather, owned_px, render_progressive
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fg = FrameGather(W, H, rank, world, cb)
+    tile = torch.zeros(fg.maxcols * H, dtype=torch.int32)
+    sc = _OracleTileScene(pyoracle.golden_scene("cornell_box_path"), tile, W, H, owned_px(W, rank, world, cb))
+
+    def keep(p, img):
+        np.save(os.path.join(outdir, f"pass{p}.npy"), FrameGather.to_rgba8(img))
+
+    render_progressive(sc, fg, tile, keep, timelimit_ms=0.0, host_tiles=True, width=W, height=H, spp=spp, max_depth=8,
+                       kind=1, seed=5, x_offset=rank, x_delt=world)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 8), (3, 4)])
+def test_gloo_progressive_previews(tmp_path, world, cb):
+    """tiles.render_progressive on CPU ranks: one broadcast per pass keeps the ranks' gathers in step, and
+    each pass's gathered preview is the single-process spp = p + 1 frame (oracle tiles; on the GPU the tiles
+    come from jsrt_render_device_progress, tests/test_gpu_multirank.py)."""
+    from oracle import pyoracle
+    W = H = 16
+    spp = 3
+    mp.start_processes(_progressive_worker, args=(world, _free_port(), W, H, cb, spp, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    blob = pyoracle.golden_scene("cornell_box_path")
+    for p in range(spp - 1):
+        _, ref, _ = pyoracle.render(blob, W, H, p + 1, 8, 1, 5, 0, 1, threads=1)
+        assert np.array_equal(np.load(os.path.join(tmp_path, f"pass{p}.npy")), ref), f"pass {p}"
