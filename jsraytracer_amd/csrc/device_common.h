@@ -345,7 +345,7 @@ __device__ __forceinline__ F3 sdf_xrep(const T *k, F3 P) {
     for (int i = 0; i < 3; ++i) {
         const double s = k[i], inv = k[3 + i], a = (double)pc[i] + s / 2;
         const double q = floor(inv != 0.0 ? a * inv : a / s);
-        r[i] = (float)(to_precision8(a - (q * s)) - s / 2);  // math.js:27
+        r[i] = (float)(to_precision8_sl(a - (q * s)) - s / 2);  // math.js:27 (branch-free form, js_number.h)
     }
     return f3(r[0], or0(r[1]), or0(r[2]));
 }
