@@ -157,6 +157,37 @@ __host__ __device__ inline double to_precision8(double v) {
     return to_precision8_exact(v);
 }
 
+// to_precision8 without branches for 1e-15 <= |v| < 1e8 (the SDF repetition range and every checkerboard
+// value), the same IEEE operations as the fast path above: the decade estimate e10 from the binary exponent
+// is floor(log10 |v|) or one less, so the scaled value of the estimate and of the decade above are both
+// formed and the one in [1e7, 1e8] kept (the fast path's loop, unrolled); the parse multiplies by 10^max(k2,
+// 0) (exact: n * 10 < 2^53) and divides by 10^max(-k2, 0) (a division by 1 is exact), one IEEE division
+// either way.  Per lane this is straight-line code: no divergent branches, whose exec-mask bookkeeping made
+// the SDF march SALU-heavy.  Bit-identical to to_precision8 (tests/test_js_number.py).
+__host__ __device__ inline double to_precision8_sl(double v) {
+    const double x = fabs(v);
+    int ex;
+    (void)frexp(x, &ex);
+    const int e10 = (int)floor((double)(ex - 1) * 0.30102999566398120);
+    if (!(x >= 1e-15 && x < 1e8) || e10 < -15) return to_precision8(v);  // (also 0, NaN, +-inf)
+    const int kA = 7 - e10;  // 0..22 for e10 in [-15, 7]
+    const double PA = pow10_exact(kA), PB = pow10_exact(kA > 0 ? kA - 1 : 0);
+    const double pA = x * PA, errA = fma(x, PA, -pA);
+    // the estimate was a decade low when the scaled value reaches 1e8 (the fast path's second iteration)
+    const bool hi = kA > 0 && (pA > 1e8 || (pA == 1e8 && errA >= 0));
+    const double pB = x * PB, errB = fma(x, PB, -pB);
+    const double p = hi ? pB : pA, err = hi ? errB : errA;
+    int e = hi ? e10 + 1 : e10;
+    const double r = floor(p), fr = p - r;
+    double n = r + ((fr > 0.5 || (fr == 0.5 && err >= 0)) ? 1.0 : 0.0);
+    const bool carry = n == 1e8;
+    n = carry ? 1e7 : n;
+    e += carry ? 1 : 0;
+    const int k2 = e - 7;
+    const double res = (n * pow10_exact(k2 > 0 ? k2 : 0)) / pow10_exact(k2 < 0 ? -k2 : 0);
+    return v < 0 ? -res : res;
+}
+
 __host__ __device__ inline double js_fmod(double a, double b) {  // math.js:27
     return to_precision8(a - (floor(a / b) * b));
 }

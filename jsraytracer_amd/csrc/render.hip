@@ -344,11 +344,15 @@ Wavefront::~Wavefront() {
 }
 
 // The schedule of a scene's frames: chain when no node can have two children; otherwise the hybrid chain
-// (side chains for second children) unless JSRT_HYBRID=0 asks for the tree schedule.
+// (side chains for second children) for flat scenes, the tree for BVH / SDF scenes (JSRT_HYBRID=0/1 forces
+// one).  A/B on MI355X (profiles/r04_s6_ab.txt): cornell hybrid 493.8 vs tree 466.3 Ms/s; bunny 518.4 vs
+// 555.7, dragon 785.4 vs 792.5, SDF_Menger 112.8 vs 116.1 -- the tree's octant-sorted appends keep BVH
+// casts coherent, and its compaction suits sky-heavy scenes.
 int schedule_of(const DScene &S) {
     if (S.max_children <= 1) return SCHED_CHAIN;
     const char *hy = getenv("JSRT_HYBRID");
-    return (hy && hy[0] == '0') ? SCHED_TREE : SCHED_HYBRID;
+    if (hy) return hy[0] == '0' ? SCHED_TREE : SCHED_HYBRID;
+    return S.profile == PF_ANALYTIC ? SCHED_HYBRID : SCHED_TREE;
 }
 constexpr size_t HYBRID_POOL_FACTOR = 2;  // initial hybrid side-chain slots: paths x factor / 4
 

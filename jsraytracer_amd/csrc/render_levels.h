@@ -656,8 +656,10 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         if (CHAIN) i = live ? chain_slot(W, L, t) : 0u;
     }
     int hp = -1, b = 0;  // b: the hit's bucket
-    if (live && W.prim[i] != NO_RAY) {
-        const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
+    // the ray is loaded together with its prim word (one memory round trip, not two dependent ones)
+    const int32_t pin = W.prim[i];
+    const F3 o = f3(W.ox[i], W.oy[i], W.oz[i]), d = f3(W.dx[i], W.dy[i], W.dz[i]);
+    if (live && pin != NO_RAY) {
         const Hit h = world_cast<PF, false>(S, o, d, minD, DINF, true);
         W.t[i] = h.t;
         W.prim[i] = h.prim;

@@ -5,6 +5,9 @@
 extern "C" void tp8_fast(const double *x, double *out, long n) {
     for (long i = 0; i < n; ++i) out[i] = jsrt::to_precision8(x[i]);
 }
+extern "C" void tp8_sl(const double *x, double *out, long n) {
+    for (long i = 0; i < n; ++i) out[i] = jsrt::to_precision8_sl(x[i]);
+}
 extern "C" void tp8_exact(const double *x, double *out, long n) {
     for (long i = 0; i < n; ++i) out[i] = jsrt::to_precision8_exact(x[i]);
 }
