@@ -741,15 +741,10 @@ __device__ __forceinline__ double prim_intersect(const DScene &S, const PT &P, F
 }
 
 // BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
-//
-// Visit order is the reference's: a node's greater child, its whole subtree, then its lesser child
-// (aggregates.js:221-222), so closest-hit ties break the same way.  The greater child is visited next in
-// a register (the node just opened needs no stack round trip); only lesser children wait on the stack.
-// FAST (the instance's leaves are all identity-transform triangle Primitives, DInst::count): leaves test
-// the leaf-ordered triangle copies directly, in a loop of their own.
-template <int PF, bool ANY, bool FAST>
-__device__ __forceinline__ Hit bvh_walk(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
+template <int PF, bool ANY>
+__device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
     Hit best{DINF, -1, I.ctx};
+    const bool fast = I.count != 0;
     // Traversal stack in LDS, one column per lane ([entry * blockDim + lane]: lanes at the same depth
     // hit distinct banks): S.bvh_stack entries (deepest node + 2 >= the D + 1 a greater-first
     // traversal can hold) of the launch's dynamic LDS (bvh_lds_bytes).  A per-lane array would live
@@ -761,9 +756,11 @@ __device__ __forceinline__ Hit bvh_walk(const DScene &S, const DInst &I, F3 o, F
     const float fmin_d = (float)minD;
     float flim = (float)maxD;  // (float)min(maxD, best)
     int sp = 0;
-    int cur = I.first;
-    for (;;) {
-        const DBvhNode N = S.bvh[cur];
+    stack[0] = I.first;
+    ++sp;
+    while (sp > 0) {
+        --sp;
+        const DBvhNode N = S.bvh[stack[sp * stride]];
 #ifndef JSRT_NO_BOX_FILTER
         int en = box_enter_f32(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, br, fmin_d, flim);
 #else
@@ -774,36 +771,28 @@ __device__ __forceinline__ Hit bvh_walk(const DScene &S, const DInst &I, F3 o, F
             en = aabb_slab(N.cx, N.cy, N.cz, N.hx, N.hy, N.hz, o, d, minD, maxD, tmn, tmx) && tmn <= maxD &&
                  tmx >= minD && tmn <= best.t;
         }
-        if (en && N.b >= 0) {  // internal: the lesser child waits, the greater one is next
-            stack[sp * stride] = N.a;
-            ++sp;
-            cur = N.b;
-            continue;
-        }
-        if (en) {  // leaf
-            const int cnt = ~N.b;
-            for (int k = 0; k < cnt; ++k) {
-                double t;
-                if (FAST) t = tri_intersect(S.ltris[N.a + k], o, d);  // leaf-ordered copy: no index load
-                else t = prim_intersect<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp, fmin(maxD, best.t));
-                if (t > minD && t < maxD && t < best.t) {
-                    best.t = t;
-                    best.prim = S.leaf_prims[N.a + k];
-                    if (ANY) return best;
-                    flim = (float)fmin(maxD, best.t);
+        if (en) {
+            if (N.b < 0) {
+                const int cnt = ~N.b;
+                for (int k = 0; k < cnt; ++k) {
+                    double t;
+                    if (fast) t = tri_intersect(S.ltris[N.a + k], o, d);  // leaf-ordered copy: no index load
+                    else t = prim_intersect<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp, fmin(maxD, best.t));
+                    if (t > minD && t < maxD && t < best.t) {
+                        best.t = t;
+                        best.prim = S.leaf_prims[N.a + k];
+                        if (ANY) return best;
+                        flim = (float)fmin(maxD, best.t);
+                    }
                 }
+            } else {
+                stack[sp * stride] = N.a;  // lesser, visited after the greater subtree
+                stack[(sp + 1) * stride] = N.b;
+                sp += 2;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur = stack[sp * stride];
     }
     return best;
-}
-template <int PF, bool ANY>
-__device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F3 d, double minD, double maxD, bool transp) {
-    if ((PF & PF_TRI) && I.count != 0) return bvh_walk<PF, ANY, true>(S, I, o, d, minD, maxD, transp);
-    return bvh_walk<PF, ANY, false>(S, I, o, d, minD, maxD, transp);
 }
 
 // Aggregate / BVH instance below the top level (aggregates.js:14-18): members flattened in DFS
