@@ -174,9 +174,20 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, WArgs W) {
 // in slot[i]; children of the last level are black without a cast), materials.js:277-330
 __device__ __forceinline__ F3 resolve_chain(const RenderArgs &A, const WArgs &W, uint32_t c, int s) {
     F3 v = f3(0, 0, 0);
-    for (int L = W.endl[c]; L >= s; --L) {
+    const int end = W.endl[c];
+    // the node records of the chain's levels, loaded before the bottom-up pass (their addresses do not
+    // depend on it): up to 8 levels' loads in flight at once instead of one dependent round trip per level
+    constexpr int PRE = 8;
+    float4 pre[PRE];
+#pragma unroll
+    for (int k = 0; k < PRE; ++k)
+        if (s + k <= end) pre[k] = W.node[(uint32_t)(s + k) * W.cap + c];
+    for (int L = end; L >= s; --L) {
         const uint32_t i = (uint32_t)L * W.cap + c;
-        const float4 nd = W.node[i];
+        float4 nd = L - s < PRE ? pre[0] : W.node[i];
+#pragma unroll
+        for (int k = 1; k < PRE; ++k)
+            if (L - s == k) nd = pre[k];
         const uint32_t info = f2u(nd.w);
         if (info & INFO_MISS) {
             v = f3(nd.x, nd.y, nd.z);
@@ -200,8 +211,7 @@ __device__ __forceinline__ F3 resolve_chain(const RenderArgs &A, const WArgs &W,
 // first.
 __global__ __launch_bounds__(256) void k_resolve_side(RenderArgs A, WArgs W, int s) {
     if (W.lvl[LVL_FLAG]) return;
-    uint32_t lo = W.npaths;
-    for (int j = 1; j < s; ++j) lo += W.lvl[2 * j + 1];
+    const uint32_t lo = side_base(W, s);
     const uint32_t c = lo + blockIdx.x * 256 + threadIdx.x;
     if (c >= lo + W.lvl[2 * s + 1]) return;
     const F3 v = resolve_chain(A, W, c, s);
@@ -747,7 +757,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     if (!h_lvl[LVL_FLAG] && !h_lvl[LVL_UNDER]) {
                         if (wf.frac.size() < (size_t)A.max_depth) wf.frac.assign(A.max_depth, 0.0);
                         for (int L = 0; L < A.max_depth; ++L)
-                            wf.frac[L] = std::max(wf.frac[L], (double)h_lvl[hybrid ? 2 * L : L] / (double)Wb.npaths);
+                            wf.frac[L] = std::max(wf.frac[L], (double)(hybrid ? h_lvl[2 * L] + h_lvl[2 * L + 1] : h_lvl[L]) / (double)Wb.npaths);
                     }
                 }
             }

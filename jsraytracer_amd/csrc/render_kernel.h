@@ -45,11 +45,11 @@ constexpr int INFO_NCHILD_SHIFT = 2;
 //         records are level-major [L * cap + q]; the child ray replaces its parent's ray.
 //         hybrid chain (branching materials, W.hybrid): the same, and a node's second child starts a
 //         side chain in a slot appended after the paths (the chains started at level s have the ids
-//         npaths + [side(< s), side(<= s))).  Level L > 0 visits only its live chains, listed by
-//         k_shade(L - 1) (list[L & 1]).  Counts: the 64-bit word lvl[2L, 2L + 1] = {live chains of level L,
-//         side chains started at L}, appended with one 64-bit atomic per block.  A chain's last level is
-//         endl[slot].  A side chain's colour is resolved bottom-up before its parent's and left in
-//         slot[parent node] (k_resolve_side).
+//         npaths + [side(< s), side(<= s))).  Level L > 0 visits only its live chains: those that continue
+//         from L - 1, listed by k_shade(L - 1) (list[L & 1]), then the side chains started at L.  Counts:
+//         the 64-bit word lvl[2L, 2L + 1] = {chains continuing into L, side chains started at L}, appended
+//         with one 64-bit atomic per block.  A chain's last level is endl[slot].  A side chain's colour is
+//         resolved bottom-up before its parent's and left in slot[parent node] (k_resolve_side).
 //   tree  (branching materials): rays and nodes share pool slots; level L occupies
 //         [base_L, base_L + count_L) with counts on the device; children are appended.
 struct WArgs {

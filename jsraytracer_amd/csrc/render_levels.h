@@ -210,17 +210,27 @@ __device__ __forceinline__ LevelRange level_range(const WArgs &W, int L) {
     return LevelRange{b, W.lvl[L]};
 }
 // Chain schedule: level L's node records start at L * cap.  It visits count chains: every path (level 0,
-// and every level without side chains), else the hybrid chain's live chains of level L (lvl[L], listed)
+// and every level without side chains), else the hybrid chain's live chains of level L: the chains that
+// continue from level L - 1 (listed, lvl[2L]) and then the side chains that start at L (lvl[2L + 1], ids
+// contiguous).  Keeping the new side chains out of the list keeps every wave's slots in one run: a side
+// chain interleaved with its parent's neighbours cost each 4-B SoA store of its wave a cache line more.
 __device__ __forceinline__ LevelRange chain_level(const WArgs &W, int L) {
     const uint32_t base = (uint32_t)L * W.cap;
     if (!W.hybrid) return LevelRange{base, W.npaths};
     if (W.lvl[LVL_FLAG]) return LevelRange{base, 0u};
-    return LevelRange{base, W.lvl[2 * L]};  // (the low word of level L's count pair)
+    return LevelRange{base, W.lvl[2 * L] + W.lvl[2 * L + 1]};
+}
+// the first id of the side chains that start at level L (ids of earlier starts below it)
+__device__ __forceinline__ uint32_t side_base(const WArgs &W, int L) {
+    uint32_t c = W.npaths;
+    for (int j = 1; j < L; ++j) c += as_const(W.lvl)[2 * j + 1];  // (words no kernel of level >= L changes)
+    return c;
 }
 // the chain slot of level L's t-th visited chain
 __device__ __forceinline__ uint32_t chain_slot(const WArgs &W, int L, uint32_t t) {
     if (!W.hybrid || L == 0) return t;
-    return ((L & 1) ? W.list1 : W.list0)[t];
+    const uint32_t nc = as_const(W.lvl)[2 * L];
+    return t < nc ? ((L & 1) ? W.list1 : W.list0)[t] : side_base(W, L) + (t - nc);
 }
 
 // shadow hand-off plane flags (store_hand)
@@ -769,14 +779,13 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         else
             at = block_append<256>(W.lvl + L + 1, nc);
     } else if (W.hybrid) {
-        // the chain continues into level L + 1 (its first child), and a second child starts a side chain:
-        // both enter level L + 1's list; the side chain takes the next id of the side chains started at L + 1
-        // (after npaths and the side chains started at levels 1..L: read here, before the first store, as a
-        // load behind the stores would wait for all of them)
+        // the chain continues into level L + 1 (its first child: an entry in level L + 1's list), and a
+        // second child starts a side chain, the next id of the side chains started at L + 1 (after npaths and
+        // those started at levels 1..L: read here, before the first store, as a load behind the stores would
+        // wait for all of them)
         const int side = (child_depth > 0 && nchild > 1) ? 1 : 0, cont = (child_depth > 0 && nchild > 0) ? 1 : 0;
-        block_append2(W.lvl + 2 * (L + 1), cont + side, side, at, side_at);
-        side_at += W.npaths;
-        for (int j = 1; j <= L; ++j) side_at += as_const(W.lvl)[2 * j + 1];  // (scalar loads: stable words)
+        block_append2(W.lvl + 2 * (L + 1), cont, side, at, side_at);
+        side_at += side_base(W, L + 1);
     }
     // ---- stores ----
     if (prim == NO_RAY) {
@@ -825,11 +834,10 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         }
         if (W.hybrid && child_depth > 0 && nchild > 1) {  // the second child's side chain
             const uint32_t c = side_at;  // npaths + side(< L + 1) + this chain's offset
-            if (c >= W.cap || at + 1 >= W.cap) {
+            if (c >= W.cap) {
                 W.lvl[LVL_FLAG] = 1u;  // out of chain slots: the host redoes the frame with more
                 return;
             }
-            next[at + 1] = c;
             W.ox[c] = out.h.pos.x; W.oy[c] = out.h.pos.y; W.oz[c] = out.h.pos.z;
             W.dx[c] = ch1.dir.x; W.dy[c] = ch1.dir.y; W.dz[c] = ch1.dir.z;
             W.addr[c] = mix32(out.h.addr, 2u);
