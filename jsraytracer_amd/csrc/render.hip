@@ -610,7 +610,10 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         if (hybrid && cap * (size_t)depth >= ((size_t)1 << 32)) { e = hipErrorOutOfMemory; break; }  // u32 node index
         const size_t pool = chain ? cap : paths * wf.pool_factor, level_cap = chain ? cap : pool / 2;
         int group = 1;
-        if (ns > 1 && ns <= 64)
+        // k_shadow: a node's light samples on `group` lanes (one each), or all on one lane (group 1: more than
+        // 64 samples, or JSRT_SHADOW_SERIAL=1, an A/B knob)
+        const char *ss = getenv("JSRT_SHADOW_SERIAL");
+        if (ns > 1 && ns <= 64 && !(ss && ss[0] == '1' && !persist))
             while (group < ns) group *= 2;
         // hand-off slots: one per node of a level; level 0 holds all `paths` camera rays, the
         // deeper levels at most level_cap (k_shade poisons the batch before writing past it)

@@ -962,7 +962,7 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     bool in = q < count;
     const float4 *hp = W.hand + (in ? q : 0u);
     uint32_t mi = 0;  // the node's shadow-root mask (grid cell of its hit point)
-    if (!SERIAL && W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
+    if (W.bucket) {  // hand-off slot q of the level's lit nodes (all filled)
         in = q < as_const(W.bkt + (size_t)L * BKT_LEVEL)[3 * BKT_K];
         const uint32_t h = in ? q : 0u;
         q = W.hnode[h];
@@ -972,14 +972,14 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
     // point in one grid cell -- the hand-off is bucketed by cell, so nearly every wave -- the world loop
     // visits only the roots a shadow segment from that cell can meet.
     uint64_t mask = ~0ull;
-    if (!SERIAL && W.bucket && W.bucket_grid && S.grid_masked) {
+    if (W.bucket && W.bucket_grid && S.grid_masked) {
         const uint64_t on = __ballot(in);
         if (on) {
             const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mi, __builtin_ctzll(on));
             if (!__ballot(in && mi != m0) && m0 <= (uint32_t)S.grid_cells) mask = as_const(S.grid_mask)[m0];
         }
     }
-    if (CHAIN && (SERIAL || !W.bucket) && in) q = chain_slot(W, L, q);  // hand-off in level order: the chain's slot
+    if (CHAIN && !W.bucket && in) q = chain_slot(W, L, q);  // hand-off in level order: the chain's slot
     const uint32_t i = base + (in ? q : 0u);
     const float4 nd = W.node[i];
     const bool lit = in && (f2u(nd.w) & INFO_LIT);
@@ -991,7 +991,7 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
             const DLight &Lt = S.lights[li];
             const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
             F3 light_color = f3(0, 0, 0);
-            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k));
+            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k, mask));
             if (n > 0) ret = add(ret, scale(light_color, Lt.inv_n));  // times(1 / samples)
         }
         W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
@@ -1221,7 +1221,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                         hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN, false>),
                                            dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN, false>, ne)), dim3(256), 0, st, S, W, L);
                     hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
-                } else if (W.ns <= 64)
+                } else if (W.ns <= 1 || W.group > 1)
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
                 else
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
