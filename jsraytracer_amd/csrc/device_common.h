@@ -325,13 +325,45 @@ __device__ __forceinline__ const CONST_AS T *as_const(const T *p) {
 // BoxSDF.distanceComp (sdf.js:276-279): q = p.abs().minus(size).to4(0);
 // Vec.max(q, 0).norm() + min(max(q0, q1, q2), 0)
 template <class T>
-__device__ __forceinline__ double sdf_box(const T *k, F3 P) {
+JSRT_HD double sdf_box(const T *k, F3 P) {
     const float qx = fabsf(P.x) - (float)k[0];
     const float qy = or0(fabsf(P.y) - (float)k[1]);
     const float qz = or0(fabsf(P.z) - (float)k[2]);
     // Math.max / Math.min of f32 values are f32 values: evaluated in f32 (js_maxf)
     const F3 m = f3(js_max0f(qx), js_max0f(qy), js_max0f(qz));
     return sqrt(dot3(m, m)) + (double)js_min0f(js_maxf(js_maxf(qx, qy), qz));
+}
+
+// UnionSDF of n BoxSDFs (k: 4 doubles apart), Math.min(d_0, ..., d_n-1) (sdf.js:83-85), with ONE square
+// root.  A box's distance is sqrt(a) + c, a = |max(q, 0)|^2 (f64), c = min(max(q), 0) (f32):
+//   outside (a > 0): c is +0 and the distance sqrt(a) > 0;  inside or on it (a == 0): 0 + c <= 0.
+// So an inside box's distance is below every outside one, and among outside boxes the correctly rounded
+// square root is monotone: min_i RN(sqrt(a_i)) = RN(sqrt(min_i a_i)).  The minimum is therefore the
+// smallest inside distance if there is one, else the root of the smallest a -- bit for bit Math.min's
+// value (no -0 arises: +0 + -0 is +0), with a NaN from any box kept (tests/test_sdf_box.py).
+template <class T>
+JSRT_HD double sdf_minbox(const T *k, int n, F3 P) {
+    double amin = __builtin_inf(), din = 0.0;
+    bool inside = false, nan = false;
+    for (int i = 0; i < n; ++i) {
+        const T *b = k + 4 * i;
+        const float qx = fabsf(P.x) - (float)b[0];
+        const float qy = or0(fabsf(P.y) - (float)b[1]);
+        const float qz = or0(fabsf(P.z) - (float)b[2]);
+        const F3 m = f3(js_max0f(qx), js_max0f(qy), js_max0f(qz));
+        const double a = dot3(m, m);
+        const float c = js_min0f(js_maxf(js_maxf(qx, qy), qz));
+        nan = nan || a != a || c != c;
+        if (a == 0.0) {
+            const double d = 0.0 + (double)c;
+            din = inside ? (d < din ? d : din) : d;
+            inside = true;
+        } else {
+            amin = a < amin ? a : amin;
+        }
+    }
+    const double r = inside ? din : sqrt(amin);
+    return nan ? __builtin_nan("") : r;
 }
 
 // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473): Math.fmod(p + s/2, s) - s/2 per axis.
@@ -452,12 +484,9 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
             break;
         }
         case SOP_XREP: P = sdf_xrep(K + ia, P); break;
-        case SOP_MINBOX: {  // BOX x ib, MIN ib
-            double r = sdf_box(K + ia, P);
-            for (int i = 1; i < ib; ++i) r = js_min(r, sdf_box(K + ia + 4 * i, P));
-            dst.set(dsp++, r);
+        case SOP_MINBOX:  // BOX x ib, MIN ib
+            dst.set(dsp++, sdf_minbox(K + ia, ib, P));
             break;
-        }
         case SOP_XMATS:  // TPUSH XMAT TPOP_MUL
             P = xf_point(K + ia, P);
             sst.set(ssp - 1, sst.get(ssp - 1) * (1.0 * K[ib]));

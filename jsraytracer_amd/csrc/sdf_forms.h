@@ -25,15 +25,13 @@ __device__ __forceinline__ double sdf_form_runion(const KT *K, const CT *code, i
     const int iters = uni(code[pc + 3].a);
     const int xm = uni(code[pc + 4].a), xs = uni(code[pc + 4].b), xr = uni(code[pc + 4].pad);
     const int u1 = uni(code[pc + 5].a), un1 = uni(code[pc + 5].b);
-    double d1 = sdf_box(K + u0, P);
-    for (int i = 1; i < un0; ++i) d1 = js_min(d1, sdf_box(K + u0 + 4 * i, P));
+    double d1 = sdf_minbox(K + u0, un0, P);
     double s = 1.0;
     F3 Q = P;
     for (int it = 0; it < iters; ++it) {
         Q = sdf_xrep(K + xr, xf_point(K + xm, Q));
         s = s * (1.0 * (1.0 * K[xs]));
-        double d = sdf_box(K + u1, Q);
-        for (int i = 1; i < un1; ++i) d = js_min(d, sdf_box(K + u1 + 4 * i, Q));
+        const double d = sdf_minbox(K + u1, un1, Q);
         d1 = js_min(d1, d * s);
     }
     return d1;
