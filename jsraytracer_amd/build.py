@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libjsrt.so")
 PROFILES = {"analytic": 0, "mesh": 9, "sdf": 4, "all": 15}  # device_scene.h PF_ANALYTIC / PF_MESH / PF_SDF / PF_ALL
-HEADERS = ["device_common.h", "js_number.h", "device_scene.h", "render_kernel.h", "render_levels.h", "scene_load.h", "sdf_forms.h",
+HEADERS = ["device_common.h", "fdlibm.h", "js_number.h", "device_scene.h", "render_kernel.h", "render_levels.h", "scene_load.h", "sdf_forms.h",
            "sdf_program.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("JSRT_OFFLOAD_ARCH", "gfx950")

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "device_scene.h"
+#include "fdlibm.h"
 #include "js_number.h"
 
 // building blocks also compiled for the host (tests/native: filter-vs-exact checks on the CPU)
@@ -174,10 +175,49 @@ JSRT_HD F3 xf_dir(const T *m, F3 d) {  // w = 0: the 4th term only adds a zero
 JSRT_HD F3 ray_point(F3 o, F3 d, double t) {
     return f3(o.x + (float)((double)d.x * t), o.y + (float)((double)d.y * t), o.z + (float)((double)d.z * t));
 }
-// Math.sin and Math.cos of one argument: OCML's sincos runs the argument reduction and the polynomial
-// pair once; its two results are bit for bit those of its sin and cos (both select from the same
-// reduction and the same sin/cos polynomial pair, ocml.bc __ocml_{sin,cos,sincos}_f64)
-__device__ __forceinline__ void sin_cos(double x, double &s, double &c) { sincos(x, &s, &c); }
+// Math.sin and Math.cos of one argument: V8's own algorithm (fdlibm.h, pinned bit for bit to node's results
+// on 3.3 M arguments, tests/test_fdlibm.py), one argument reduction for the pair.  (OCML's sin / cos / acos
+// differ from V8 in the last bit on ~3 % of arguments, as glibc's do.)
+__device__ __forceinline__ void sin_cos(double x, double &s, double &c) { fdlibm::sin_cos(x, s, c); }
+// Vec.spherePick() (math.js:180-185): theta = 2 pi r0, phi = acos(2 r1 - 1), the point (cos theta sin phi,
+// cos phi, sin theta sin phi) as f32, with V8's sin / cos / acos (fdlibm.h).  Only the three f32 roundings
+// reach the image, so OCML's sincos and acos (inlined twice, fdlibm costs k_shade ~70 spilled VGPRs) are
+// evaluated first and kept when every value within SPHERE_PICK_EPS = 2^-44 of each product rounds to the
+// same f32: tests/test_gpu_trig.py bounds |OCML - V8| by 2^-50 on the spherePick arguments of node's fixture,
+// so a product is within 3 * 2^-50 + 2^-52 of V8's, 19x inside the margin, and a kept result is V8's.  The
+// rest (|value| below ~2^-20, or within 2^-44 of an f32 rounding boundary: about one pick in 10^5) are
+// recomputed with fdlibm, out of line.
+constexpr double SPHERE_PICK_EPS = 0x1p-44;
+__device__ __forceinline__ bool f32_stable(double d) {
+    return (float)(d - SPHERE_PICK_EPS) == (float)(d + SPHERE_PICK_EPS);
+}
+struct SinCos2 {
+    double st, ct, sp, cp;
+};
+__device__ __attribute__((noinline)) inline SinCos2 sphere_pick_exact(double theta, double a) {
+    SinCos2 r;
+    fdlibm::sin_cos(theta, r.st, r.ct);
+    fdlibm::sin_cos(fdlibm::acos(a), r.sp, r.cp);
+    return r;
+}
+template <class R>
+__device__ __forceinline__ F3 sphere_pick(R &rng) {
+    const double theta = 2.0 * JS_PI * rng.next();
+    const double a = 2.0 * rng.next() - 1.0;
+    double sin_t, cos_t, sin_phi, cos_phi;
+#ifdef JSRT_EXACT_TRIG  // A/B: fdlibm only
+    const bool fast = false;
+#else
+    sincos(theta, &sin_t, &cos_t);
+    sincos(::acos(a), &sin_phi, &cos_phi);
+    const bool fast = f32_stable(cos_t * sin_phi) && f32_stable(cos_phi) && f32_stable(sin_t * sin_phi);
+#endif
+    if (__builtin_expect(!fast, 0)) {  // out of line: the hot path keeps OCML's register footprint
+        const SinCos2 r = sphere_pick_exact(theta, a);
+        sin_t = r.st, cos_t = r.ct, sin_phi = r.sp, cos_phi = r.cp;
+    }
+    return f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
+}
 // Vec.cartesianToSpherical (math.js:189-193)
 __device__ __forceinline__ void cart_to_sph(F3 n, float &u, float &v) {
     u = (float)(0.5 + atan2((double)n.z, (double)n.x) / (2 * JS_PI));
@@ -1176,12 +1216,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
     } else {  // RandomSampleAreaLight.sampleIterator (lights.js:80-92)
         F3 local;
         if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Vec.spherePick().to4(1)
-            const double theta = 2.0 * JS_PI * rng.next();
-            const double phi = acos(2.0 * rng.next() - 1.0);
-            double sin_t, cos_t, sin_phi, cos_phi;
-            sin_cos(theta, sin_t, cos_t);
-            sin_cos(phi, sin_phi, cos_phi);
-            local = f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
+            local = sphere_pick(rng);
         } else {  // Square / Circle.sampleSurface (geometry.js:295-300, 326-331)
             const double a = rng.next() - 0.5;
             const double b = rng.next() - 0.5;
@@ -1228,12 +1263,7 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
     const double probSum = dp + sp;
     if (probSum == 0) return false;
     if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
-        const double theta = 2.0 * JS_PI * rng.next();
-        const double phi = acos(2.0 * rng.next() - 1.0);
-        double sin_t, cos_t, sin_phi, cos_phi;
-        sin_cos(theta, sin_t, cos_t);
-        sin_cos(phi, sin_phi, cos_phi);
-        const F3 sp3 = f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
+        const F3 sp3 = sphere_pick(rng);
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;

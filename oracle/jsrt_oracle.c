@@ -12,9 +12,10 @@
  *     oracle/refharness/keyed_rng.js (the same substitution is applied to the reference when the
  *     golden fixtures are generated).
  * Built with -ffp-contract=off -fno-fast-math so every + - * / is one IEEE op, as in V8.
- * Transcendentals (cos, sin, acos, asin, atan2, pow) come from the C library; V8 uses fdlibm ports
- * whose results can differ in the last float64 ulp, which the f32 stores absorb (pinned by the
- * whole-image goldens, tests/test_oracle_golden.py).
+ * Math.sin, Math.cos and Math.acos are V8's fdlibm algorithms (js_fdlibm.h, bit for bit node's own results on
+ * 3.3 M arguments, tests/test_oracle_trig.py); the C library's differ in the last float64 ulp on ~3 % of
+ * arguments.  asin, atan2 (sphere UVs) and pow still come from the C library, whose last-ulp differences the
+ * f32 stores absorb (pinned by the whole-image goldens, tests/test_oracle_golden.py).
  */
 #define _GNU_SOURCE
 #include "jsrt_oracle.h"
@@ -27,6 +28,7 @@
 #include <string.h>
 
 #include "../include/jsrt_scene.h"
+#include "js_fdlibm.h"
 
 #define JS_PI 3.141592653589793
 
@@ -849,9 +851,9 @@ static Vec sample_surface(Ctx *C, uint32_t kind) {
         return vof4(a, b, 0, 1);
     }
     /* Sphere: Vec.spherePick().to4(1) (geometry.js:446-448, math.js:180-188) */
-    const double theta = 2.0 * JS_PI * rnd(C), phi = acos(2.0 * rnd(C) - 1.0);
-    const double sin_phi = sin(phi);
-    return vto4(vof3(cos(theta) * sin_phi, cos(phi), sin(theta) * sin_phi), 1);
+    const double theta = 2.0 * JS_PI * rnd(C), phi = js_acos(2.0 * rnd(C) - 1.0);
+    const double sin_phi = js_sin(phi);
+    return vto4(vof3(js_cos(theta) * sin_phi, js_cos(phi), js_sin(theta) * sin_phi), 1);
 }
 
 static void phong_base_factors(Ctx *C, const jsrt_rec_material *M, MData *d) { /* materials.js:210-238 */
@@ -994,9 +996,9 @@ static Scatter path_scatter(Ctx *C, const jsrt_rec_material *M, int has_R, Vec R
     if (probSum == 0) return s;
     if (rnd(C) < (diffuseProb / probSum)) {
         /* scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized() (materials.js:438-440) */
-        const double theta = 2.0 * JS_PI * rnd(C), phi = acos(2.0 * rnd(C) - 1.0);
-        const double sin_phi = sin(phi);
-        Vec sp = vof3(cos(theta) * sin_phi, cos(phi), sin(theta) * sin_phi);
+        const double theta = 2.0 * JS_PI * rnd(C), phi = js_acos(2.0 * rnd(C) - 1.0);
+        const double sin_phi = js_sin(phi);
+        Vec sp = vof3(js_cos(theta) * sin_phi, js_cos(phi), js_sin(theta) * sin_phi);
         s.ok = 1;
         s.dir = vnormalized(vplus(N, vto4(sp, 0)));
         s.col = vtimes(d->diffusivity, 1 / JS_PI);
@@ -1194,7 +1196,7 @@ static Ray camera_ray(Ctx *C, double x, double y) {
     Ray r = {mat_column(&T, 3), mat_vec(&T, dir)};
     if (K->kind == JSRT_CAMERA_DOF) {
         const double a = rnd(C) * 2 * JS_PI, rr = sqrt(rnd(C)); /* Vec.circlePick (math.js:175-179) */
-        Vec cp = vof2(rr * cos(a), rr * sin(a));
+        Vec cp = vof2(rr * js_cos(a), rr * js_sin(a));
         Vec offset = mat_vec(&T, vto4(vtimes(cp, K->sensor_size), 0));
         r.o = vplus(r.o, offset);
         r.d = vnormalized(vminus(vtimes(r.d, K->focus_distance), offset));
@@ -1423,4 +1425,13 @@ int jsrt_oracle_sdf_distance(const void *blob, size_t blob_bytes, int32_t obj, c
     const int err = C->err;
     free(C);
     return err ? -3 : 0;
+}
+
+/* Math.sin / Math.cos / Math.acos of n arguments (tests/test_oracle_trig.py: pinned to node's results) */
+void jsrt_oracle_trig(const double *x, double *out, long n) {
+    for (long i = 0; i < n; ++i) {
+        out[3 * i] = js_sin(x[i]);
+        out[3 * i + 1] = js_cos(x[i]);
+        out[3 * i + 2] = js_acos(x[i]);
+    }
 }
