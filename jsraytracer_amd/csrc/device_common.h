@@ -266,7 +266,7 @@ struct BoxRay {       // per ray: the f32 reciprocals and the reference's epsilo
     float inv[3];
     uint32_t skip;    // bit i: |d_i| <= 1e-7 (geometry.js:194, compared in f64)
 };
-__device__ __forceinline__ BoxRay box_ray(F3 d) {
+JSRT_HD BoxRay box_ray(F3 d) {
     BoxRay r;
     const float dd[3] = {d.x, d.y, d.z};
     r.skip = 0;
@@ -308,6 +308,60 @@ __device__ __forceinline__ int box_enter_f32(float cx, float cy, float cz, float
     const bool c3_false = __builtin_isfinite(flim) ? tmin - en > flim + (EPS * fabsf(flim) + TINY) : flim < 0;
     if (c3_false) return 0;
     if (tmin + en < tmax - ex && tmax - ex > fmin_d + em && c3_true) return 1;
+    return -1;
+}
+
+// Any-hit acceptance of an AABB geometry in a shadow cast (AABB.intersect, geometry.js:173-179, then
+// World.cast's minD < t < maxD; a shadow cast stops at its first accepted hit, so `best` is +inf on every
+// lane that still casts), decided in f32 with box_enter_f32's error bound: 1 = accepted (t_out = the f32
+// estimate of the distance, inside (minD, maxD) by the margin), 0 = not accepted, -1 = too close to call
+// (the caller runs the exact aabb_intersect).  The exact outcome: the slab passes (box_enter_f32's
+// conditions with lim = maxD) and t = tmin >= minD ? tmin : tmax lies in (minD, maxD), i.e.
+//   minD < tmin < maxD and tmin <= tmax,  or  tmin < minD < tmax < maxD
+// (tmin == minD gives t = minD: rejected, and too close to call here).  The six correctly rounded f64
+// divisions of the exact slab run only for a decision within 2^-21 of a boundary.
+template <class T>  // T: float in any address space
+JSRT_HD int box_any_f32(const T *c, const T *h, F3 o, const BoxRay &r, double minD, double maxD, double &t_out) {
+    constexpr float EPS = 4.76837158203125e-7f, TINY = 1e-30f;  // 2^-21
+    const float oo[3] = {o.x, o.y, o.z};
+    float tmin = -__builtin_inff(), tmax = __builtin_inff();
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float p = c[i] - oo[i];
+        if ((r.skip >> i) & 1u) {
+            out = out || fabsf(p) > h[i];  // exact: both f32
+        } else {
+            const float a = (p + h[i]) * r.inv[i], b = (p - h[i]) * r.inv[i];
+            tmin = fmaxf(tmin, fminf(a, b));
+            tmax = fminf(tmax, fmaxf(a, b));
+        }
+    }
+    if (out) return 0;
+    if (!__builtin_isfinite(tmin) || !__builtin_isfinite(tmax)) return -1;  // (also every axis skipped)
+    const float f0 = (float)minD, f1 = (float)maxD;
+    if (!__builtin_isfinite(f0)) return -1;
+    const bool inf1 = !__builtin_isfinite(f1) && f1 > 0;  // maxD = +inf: every finite t is below it
+    const float en = EPS * fabsf(tmin) + TINY, ex = EPS * fabsf(tmax) + TINY;
+    const float e0 = EPS * fabsf(f0) + TINY, e1 = inf1 ? 0.0f : EPS * fabsf(f1) + TINY;
+    if (tmin - en > f0 + e0) {  // tmin > minD: t = tmin
+        const bool lt1 = inf1 || tmin + en < f1 - e1, gt1 = !inf1 && tmin - en > f1 + e1;
+        if (gt1 || tmin - en > tmax + ex) return 0;
+        if (lt1 && tmin + en < tmax - ex) {
+            t_out = tmin;
+            return 1;
+        }
+        return -1;
+    }
+    if (tmin + en < f0 - e0) {  // tmin < minD: t = tmax
+        const bool lt1 = inf1 || tmax + ex < f1 - e1, gt1 = !inf1 && tmax - ex > f1 + e1;
+        if (tmax + ex < f0 - e0 || gt1) return 0;
+        if (tmax - ex > f0 + e0 && lt1) {
+            t_out = tmax;
+            return 1;
+        }
+        return -1;
+    }
     return -1;
 }
 
@@ -796,6 +850,108 @@ JSRT_HD double planar_intersect(int k, const T *inv, F3 o, F3 d, double minD, do
     return (dot3(p, p) <= 1) ? t : -(double)__builtin_inf();  // Circle, geometry.js:310-314
 }
 
+// Any-hit acceptance of a SimplePlane / Square / Circle in a shadow cast (planar_intersect's result accepted
+// by minD < t < maxD; `best` is +inf on every lane still casting), decided in f32: 1 = accepted (t_out = the
+// f32 estimate of the distance, inside the bounds by the margin), 0 = not accepted, -1 = too close to call
+// (the caller runs planar_intersect).  The plane distance -oz / dz is estimated as -oz * rcp(dz) (within
+// 2^-21 relative: rcp's 1 ulp and the product's rounding); the hit point p = o + (f32)(d * t), which the exact
+// path forms from the f64 distance with two f32 roundings, moves by at most 2^-18 (|d t| + |o|) per
+// component under the estimate, so a bound test decided outside that margin is the exact test's outcome.
+template <class T>
+JSRT_HD int planar_any_f32(int k, const T *inv, F3 o, F3 d, double minD, double maxD, double &t_out) {
+    constexpr float EPS = 4.76837158203125e-7f, EPSP = 3.814697265625e-6f, TINY = 1e-30f;  // 2^-21, 2^-18
+    const float oz = xf_row_point(inv + 8, o), dz = xf_row_dir(inv + 8, d);
+    if (dz == 0.0f) return 0;  // t = -inf (planar_intersect's dz == 0 case): never accepted
+#ifdef __HIP_DEVICE_COMPILE__
+    const float ta = -oz * __builtin_amdgcn_rcpf(dz);  // v_rcp_f32: within 1 ulp
+#else
+    const float ta = -oz * (1.0f / dz);  // (host build of the tests: correctly rounded, inside the same bound)
+#endif
+    const float f0 = (float)minD, f1 = (float)maxD;
+    if (!__builtin_isfinite(ta) || !__builtin_isfinite(f0) || !(fabsf(dz) >= 1e-30f)) return -1;
+    const bool inf1 = !__builtin_isfinite(f1) && f1 > 0;
+    const float et = EPS * fabsf(ta) + TINY, e0 = EPS * fabsf(f0) + TINY, e1 = inf1 ? 0.0f : EPS * fabsf(f1) + TINY;
+    if (ta + et < f0 - e0 || (!inf1 && ta - et > f1 + e1)) return 0;
+    if (!(ta - et > f0 + e0 && (inf1 || ta + et < f1 - e1))) return -1;
+    if (k == JSRT_GEOM_PLANE) {
+        t_out = ta;
+        return 1;
+    }
+    const float ox = xf_row_point(inv, o), oy = xf_row_point(inv + 4, o);
+    const float dx = xf_row_dir(inv, d), dy = xf_row_dir(inv + 4, d);
+    const double td = (double)ta;
+    const float sx = (float)((double)dx * td), sy = (float)((double)dy * td);
+    const float px = ox + sx, py = oy + sy;
+    const float ex = EPSP * (fabsf(sx) + fabsf(ox)) + TINY, ey = EPSP * (fabsf(sy) + fabsf(oy)) + TINY;
+    if (!__builtin_isfinite(px) || !__builtin_isfinite(py) || !__builtin_isfinite(ex) || !__builtin_isfinite(ey))
+        return -1;
+    if (k == JSRT_GEOM_SQUARE) {  // -0.5 <= p.x <= 0.5 && -0.5 <= p.y <= 0.5
+        if (fabsf(px) - ex > 0.5f || fabsf(py) - ey > 0.5f) return 0;
+        if (fabsf(px) + ex < 0.5f && fabsf(py) + ey < 0.5f) {
+            t_out = ta;
+            return 1;
+        }
+        return -1;
+    }
+    // Circle: dot3(p, p) <= 1, with p.z = oz + (f32)(dz t) (the residual of the plane itself)
+    const float sz = (float)((double)dz * td), pz = oz + sz;
+    const float ez = EPSP * (fabsf(sz) + fabsf(oz)) + TINY;
+    const double r2 = dot3(f3(px, py, pz), f3(px, py, pz));
+    const double m = 2.0 * ((double)fabsf(px) * ex + (double)fabsf(py) * ey + (double)fabsf(pz) * ez) +
+                     ((double)ex * ex + (double)ey * ey + (double)ez * ez) + 1e-15;
+    if (!__builtin_isfinite(r2)) return -1;
+    if (r2 - m > 1.0) return 0;
+    if (r2 + m < 1.0) {
+        t_out = ta;
+        return 1;
+    }
+    return -1;
+}
+
+// Any-hit acceptance of a Sphere in a shadow cast (sphere_static's result accepted by minD < t < maxD),
+// decided in f32: 1 / 0 / -1 as planar_any_f32.  a, b, c and the discriminant are the reference's f64
+// values (the exact path's own operations); the square root and the two quotients are estimated in f32.
+// Since a > 0, t1 >= t2 and sphere_static returns t = t2 >= minD ? t2 : t1.  Each estimate is within
+// 2^-19 (sqrt(disc) / a + |t|) of the exact quotient: the f32 roundings of b, a and the discriminant
+// (2^-24 each), sqrt and rcp (1 ulp each) and the f32 sum (2^-24 (|b| + sqrt(disc))), whose cancellation
+// term is covered by sqrt(disc) / a when it is large and by |t| ~ |b| / a when sqrt(disc) is small.
+JSRT_HD int sphere_any_f32(F3 o, F3 d, double minD, double maxD, double &t_out) {
+    constexpr float EPS = 4.76837158203125e-7f, EPSS = 1.9073486328125e-6f, TINY = 1e-30f;  // 2^-21, 2^-19
+    const double a = dot3(d, d), b = dot3(d, o), c = dot3(o, o) - 1;
+    const double big = b * b - a * c;
+    if (big < 0 || a == 0) return 0;  // sphere_static: -inf
+    if (!(big >= 1e-30) || !(a >= 1e-30) || !(a <= 1e30) || !(fabs(b) <= 1e30) || !(big <= 1e30)) return -1;
+    const float fa = (float)a, fb = (float)b;
+#ifdef __HIP_DEVICE_COMPILE__
+    const float sq = __builtin_amdgcn_sqrtf((float)big), ia = __builtin_amdgcn_rcpf(fa);
+#else
+    const float sq = sqrtf((float)big), ia = 1.0f / fa;
+#endif
+    const float t1 = (-fb + sq) * ia, t2 = (-fb - sq) * ia;
+    const float base = EPSS * (sq * ia);
+    const float e1 = base + EPSS * fabsf(t1) + TINY, e2 = base + EPSS * fabsf(t2) + TINY;
+    const float f0 = (float)minD, f1 = (float)maxD;
+    if (!__builtin_isfinite(f0)) return -1;
+    const bool inf1 = !__builtin_isfinite(f1) && f1 > 0;
+    const float em = EPS * fabsf(f0) + TINY, eM = inf1 ? 0.0f : EPS * fabsf(f1) + TINY;
+    float t, et;
+    if (t2 - e2 > f0 + em) {  // t2 > minD: t = t2
+        t = t2;
+        et = e2;
+    } else if (t2 + e2 < f0 - em) {  // t2 < minD: t = t1
+        t = t1;
+        et = e1;
+    } else {
+        return -1;
+    }
+    if (t + et < f0 - em || (!inf1 && t - et > f1 + eM)) return 0;
+    if (t - et > f0 + em && (inf1 || t + et < f1 - eM)) {
+        t_out = t;
+        return 1;
+    }
+    return -1;
+}
+
 // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast.
 // `lim` = the caller's acceptance bound min(best, maxD): every caller accepts a distance only when
 // minD < t < lim, so a planar primitive whose plane distance already fails that test may return it
@@ -807,6 +963,36 @@ __device__ __forceinline__ double prim_intersect(const DScene &S, const PT &P, F
     const int k = P.gkind;
     if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) return planar_intersect(k, P.inv, o, d, minD, lim);
     return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
+}
+
+// A Primitive's distance as a shadow cast reads it (accepted or not): for an AABB, planar or sphere geometry the f32
+// decisions above (an accepted distance is the f32 estimate, a rejected one -inf), the exact test only for
+// a decision too close to call; every other kind through prim_intersect.
+template <int PF, class PT>
+__device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F3 d, double minD, double maxD,
+                                           bool transp) {
+#ifndef JSRT_NO_ANY_FILTER
+    const int k = P.gkind;
+    double t = 0;
+    if (k == JSRT_GEOM_AABB) {
+        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+        const int dec = box_any_f32(P.center, P.half, lo, box_ray(ld), minD, maxD, t);
+        if (dec >= 0) return dec ? t : -DINF;
+        return aabb_intersect(P.center, P.half, lo, ld, minD, maxD);
+    }
+    if (k == JSRT_GEOM_PLANE || k == JSRT_GEOM_SQUARE || k == JSRT_GEOM_CIRCLE) {
+        const int dec = planar_any_f32(k, P.inv, o, d, minD, maxD, t);
+        if (dec >= 0) return dec ? t : -DINF;
+        return planar_intersect(k, P.inv, o, d, minD, maxD);
+    }
+    if (k == JSRT_GEOM_SPHERE) {
+        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+        const int dec = sphere_any_f32(lo, ld, minD, maxD, t);
+        if (dec >= 0) return dec ? t : -DINF;
+        return sphere_static(lo, ld, minD);
+    }
+#endif
+    return prim_intersect<PF>(S, P, o, d, minD, maxD, transp, maxD);
 }
 
 // BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
@@ -959,7 +1145,8 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         } else if (R.kind == INST_PRIM) {
             // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
             if (transp || R.p.casts_shadow) {
-                const double t = prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
+                const double t = ANY ? prim_any<PF>(S, R.p, o, d, minD, maxD, transp)
+                                     : prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
                 if (t > minD && t < best.t && t < maxD) {
                     best = Hit{t, R.prim, 0};
                     flim = (float)best.t;

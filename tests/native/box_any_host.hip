@@ -1,0 +1,45 @@
+// Host build of the shadow cast's AABB any-hit filter (jsraytracer_amd/csrc/device_common.h box_any_f32) for
+// the CPU tests (tests/test_box_any.py): its decisions against the exact aabb_intersect + World.cast bounds.
+#include "../../jsraytracer_amd/csrc/device_common.h"
+
+// boxes: n x 6 floats (center xyz, half xyz); rays: n x 6 floats (o xyz, d xyz).  Per case: exact[i] = 1 if the
+// reference accepts the hit (minD < t < maxD), dec[i] = box_any_f32's decision, tf[i] = its distance estimate.
+extern "C" void box_any(const float *boxes, const float *rays, long n, double minD, double maxD, int *exact,
+                        int *dec, double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *b = boxes + 6 * i, *r = rays + 6 * i;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double t = jsrt::aabb_intersect(b, b + 3, o, d, minD, maxD);
+        exact[i] = (t > minD && t < maxD) ? 1 : 0;
+        double e = 0;
+        dec[i] = jsrt::box_any_f32(b, b + 3, o, jsrt::box_ray(d), minD, maxD, e);
+        tf[i] = e;
+    }
+}
+
+// planar: n x 12 doubles (inv rows 0..2), kinds[i] (JSRT_GEOM_PLANE / SQUARE / CIRCLE), rays n x 6 floats
+extern "C" void planar_any(const double *inv, const int *kinds, const float *rays, long n, double minD, double maxD,
+                           int *exact, int *dec, double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *r = rays + 6 * i;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double t = jsrt::planar_intersect(kinds[i], inv + 12 * i, o, d, minD, maxD);
+        exact[i] = (t > minD && t < maxD) ? 1 : 0;
+        double e = 0;
+        dec[i] = jsrt::planar_any_f32(kinds[i], inv + 12 * i, o, d, minD, maxD, e);
+        tf[i] = e;
+    }
+}
+
+// spheres (unit sphere, local rays): rays n x 6 floats
+extern "C" void sphere_any(const float *rays, long n, double minD, double maxD, int *exact, int *dec, double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *r = rays + 6 * i;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double t = jsrt::sphere_static(o, d, minD);
+        exact[i] = (t > minD && t < maxD) ? 1 : 0;
+        double e = 0;
+        dec[i] = jsrt::sphere_any_f32(o, d, minD, maxD, e);
+        tf[i] = e;
+    }
+}
