@@ -399,6 +399,93 @@ JSRT_HD double tri_intersect(const DTri &T, F3 o, F3 d) {  // geometry.js:368-37
     return (b0 >= 0 && b0 <= 1 && b1 >= 0 && b1 <= 1 && b2 >= 0 && b2 <= 1) ? distance : -DINF;
 }
 
+
+// f32 reciprocal within 1 ulp (v_rcp_f32 on the device; the host build of the tests divides, inside the same
+// bound)
+JSRT_HD float rcp_f32(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
+// Any-hit acceptance of a Triangle in a shadow cast (tri_intersect's result accepted by minD < t < maxD),
+// decided in f32: 1 / 0 / -1 as planar_any_f32.  The plane distance num / denom (num and denom the exact
+// path's own f64 values) is estimated as f32(num) * rcp(f32(denom)), within 2^-20 relative; the hit point
+// then moves by at most 2^-18 (|d t| + |o|) per component (planar_any_f32), v2 = p - p0 by that plus
+// 2^-22 (|p| + |p0|), and the dots, Cramer numerators and quotients, evaluated in f32 from the f64 Gram
+// terms, carry the propagated bound plus 2^-20 of their magnitudes (at most ~8 f32 roundings of 2^-24
+// each).  A barycentric b = f32(x) is in [0, 1] whenever x is (f32 rounding is monotone and keeps 0 and
+// 1), below 0 when x < -1e-30 and above 1 when x > 1 + 2^-22; a decision outside the margins is therefore
+// the exact test's outcome.  The three correctly rounded f64 divisions run only when it is too close.
+JSRT_HD int tri_any_f32(const DTri &T, F3 o, F3 d, double minD, double maxD, double &t_out) {
+    constexpr float EPS = 4.76837158203125e-7f, EPST = 9.5367431640625e-7f, EPSP = 3.814697265625e-6f;
+    constexpr float E22 = 2.384185791015625e-7f, TINY = 1e-30f;  // 2^-21, 2^-20, 2^-18, 2^-22
+    const F3 n = f3(T.n[0], T.n[1], T.n[2]);
+    const double denom = dot3(n, d);
+    if (denom == 0) return 0;  // tri_intersect: -inf
+    const double num = T.delta - dot3(n, o);
+    const float fd = (float)denom, fn = (float)num;
+    if (!(fabsf(fd) >= 1e-30f && fabsf(fd) <= 1e30f) || !(fabsf(fn) <= 1e30f) || (fn != 0.0f && fabsf(fn) < 1e-20f))
+        return -1;
+    const float t = fn * rcp_f32(fd);
+    const float f0 = (float)minD, f1 = (float)maxD;
+    if (!__builtin_isfinite(t) || !__builtin_isfinite(f0)) return -1;
+    const bool inf1 = !__builtin_isfinite(f1) && f1 > 0;
+    const float et = EPST * fabsf(t) + TINY, e0 = EPS * fabsf(f0) + TINY, e1 = inf1 ? 0.0f : EPS * fabsf(f1) + TINY;
+    if (t + et < f0 - e0 || (!inf1 && t - et > f1 + e1)) return 0;
+    if (!(t - et > f0 + e0 && (inf1 || t + et < f1 - e1))) return -1;
+    // the hit point and v2 = p - p0, with per-component bounds
+    const float s[3] = {d.x * t, d.y * t, d.z * t}, oo[3] = {o.x, o.y, o.z};
+    float v2[3], ev[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float pk = oo[k] + s[k];
+        v2[k] = pk - T.p0[k];
+        ev[k] = EPSP * (fabsf(s[k]) + fabsf(oo[k])) + E22 * (fabsf(pk) + fabsf(T.p0[k])) + TINY;
+    }
+    const float d20 = v2[0] * T.v0[0] + v2[1] * T.v0[1] + v2[2] * T.v0[2];
+    const float d21 = v2[0] * T.v1[0] + v2[1] * T.v1[1] + v2[2] * T.v1[2];
+    const float a20 = fabsf(v2[0] * T.v0[0]) + fabsf(v2[1] * T.v0[1]) + fabsf(v2[2] * T.v0[2]);
+    const float a21 = fabsf(v2[0] * T.v1[0]) + fabsf(v2[1] * T.v1[1]) + fabsf(v2[2] * T.v1[2]);
+    const float e20 = ev[0] * fabsf(T.v0[0]) + ev[1] * fabsf(T.v0[1]) + ev[2] * fabsf(T.v0[2]) + EPST * a20 + TINY;
+    const float e21 = ev[0] * fabsf(T.v1[0]) + ev[1] * fabsf(T.v1[1]) + ev[2] * fabsf(T.v1[2]) + EPST * a21 + TINY;
+    const float d00 = (float)T.d00, d11 = (float)T.d11, d01 = (float)T.d01, fden = (float)T.denom;
+    if (!(fabsf(fden) >= 1e-30f) || !__builtin_isfinite(fden)) return -1;
+    const float ia = fabsf(rcp_f32(fden));
+    const float vn = d11 * d20 - d01 * d21, wn = d00 * d21 - d01 * d20;
+    const float mv = fabsf(d11 * d20) + fabsf(d01 * d21), mw = fabsf(d00 * d21) + fabsf(d01 * d20);
+    const float v = vn * rcp_f32(fden), w = wn * rcp_f32(fden);
+    const float ebv = (fabsf(d11) * e20 + fabsf(d01) * e21 + EPST * mv) * ia + EPST * fabsf(v) + TINY;
+    const float ebw = (fabsf(d00) * e21 + fabsf(d01) * e20 + EPST * mw) * ia + EPST * fabsf(w) + TINY;
+    const float b0 = 1.0f - v - w, eb0 = ebv + ebw + EPST * (1.0f + fabsf(v) + fabsf(w));
+    if (!__builtin_isfinite(b0) || !__builtin_isfinite(eb0) || !__builtin_isfinite(ebv) || !__builtin_isfinite(ebw))
+        return -1;
+    const float x[3] = {b0, v, w}, e[3] = {eb0, ebv, ebw};
+    bool in = true, out = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        out = out || x[k] + e[k] < -1e-30f || x[k] - e[k] > 1.0f + E22;
+        in = in && x[k] - e[k] >= 0.0f && x[k] + e[k] <= 1.0f;
+    }
+    if (out) return 0;
+    if (in) {
+        t_out = t;
+        return 1;
+    }
+    return -1;
+}
+// a Triangle's distance as a shadow cast reads it (tri_any_f32, the exact test only when too close to call)
+JSRT_HD double tri_any(const DTri &T, F3 o, F3 d, double minD, double maxD) {
+#if !defined(JSRT_NO_ANY_FILTER) && !defined(JSRT_NO_TRI_ANY)  // (-DJSRT_NO_TRI_ANY: A/B of the triangle filter)
+    double t = 0;
+    const int dec = tri_any_f32(T, o, d, minD, maxD, t);
+    if (dec >= 0) return dec ? t : -DINF;
+#endif
+    return tri_intersect(T, o, d);
+}
+
 // --------------------------------------------------------------------------------------------
 // SDF program VM (sdf_program.h).  P is the 4-vector point with w == 1.
 //
@@ -965,13 +1052,14 @@ __device__ __forceinline__ double prim_intersect(const DScene &S, const PT &P, F
     return prim_intersect_local<PF>(S, P, xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
 }
 
-// A Primitive's distance as a shadow cast reads it (accepted or not): for an AABB, planar or sphere geometry the f32
+// A Primitive's distance as a shadow cast reads it (accepted or not): for an AABB, planar, sphere or triangle geometry the f32
 // decisions above (an accepted distance is the f32 estimate, a rejected one -inf), the exact test only for
 // a decision too close to call; every other kind through prim_intersect.
 template <int PF, class PT>
 __device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F3 d, double minD, double maxD,
                                            bool transp) {
 #ifndef JSRT_NO_ANY_FILTER
+    if (!transp && !P.casts_shadow) return DINF;  // Primitive.intersect (as prim_intersect)
     const int k = P.gkind;
     double t = 0;
     if (k == JSRT_GEOM_AABB) {
@@ -985,6 +1073,8 @@ __device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F
         if (dec >= 0) return dec ? t : -DINF;
         return planar_intersect(k, P.inv, o, d, minD, maxD);
     }
+    if ((PF & PF_TRI) && k == JSRT_GEOM_TRIANGLE)
+        return tri_any(S.tris[P.gindex], xf_point(P.inv, o), xf_dir(P.inv, d), minD, maxD);
     if (k == JSRT_GEOM_SPHERE) {
         const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
         const int dec = sphere_any_f32(lo, ld, minD, maxD, t);
@@ -1031,7 +1121,9 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                 const int cnt = ~N.b;
                 for (int k = 0; k < cnt; ++k) {
                     double t;
-                    if (fast) t = tri_intersect(S.ltris[N.a + k], o, d);  // leaf-ordered copy: no index load
+                    if (fast) t = ANY ? tri_any(S.ltris[N.a + k], o, d, minD, maxD)  // leaf-ordered copy: no index load
+                                      : tri_intersect(S.ltris[N.a + k], o, d);
+                    else if (ANY) t = prim_any<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp);
                     else t = prim_intersect<PF>(S, S.prims[S.leaf_prims[N.a + k]], o, d, minD, maxD, transp, fmin(maxD, best.t));
                     if (t > minD && t < maxD && t < best.t) {
                         best.t = t;
@@ -1080,7 +1172,8 @@ __device__ __forceinline__ void nested_cast(const DScene &S, int inst, F3 o, F3 
         const int c = S.inst_child[I.first + f.next++];
         const DInst &C = S.insts[c];
         if (C.kind == INST_PRIM) {
-            const double t = prim_intersect<PF>(S, S.prims[C.prim], f.o, f.d, minD, maxD, transp, fmin(maxD, best.t));
+            const double t = ANY ? prim_any<PF>(S, S.prims[C.prim], f.o, f.d, minD, maxD, transp)
+                                 : prim_intersect<PF>(S, S.prims[C.prim], f.o, f.d, minD, maxD, transp, fmin(maxD, best.t));
             if (t > minD && t < best.t && t < maxD) {
                 best = Hit{t, C.prim, I.ctx};
                 if (ANY) return;

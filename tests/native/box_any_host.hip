@@ -43,3 +43,38 @@ extern "C" void sphere_any(const float *rays, long n, double minD, double maxD, 
         tf[i] = e;
     }
 }
+
+// triangles: n x 9 floats (3 vertices), rays n x 6 floats; the DTri fields as mesh_build.cpp computes them
+extern "C" void tri_any(const float *verts, const float *rays, long n, double minD, double maxD, int *exact, int *dec,
+                        double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *p = verts + 9 * i, *r = rays + 6 * i;
+        jsrt::DTri T{};
+        float a[3], b[3], h[3];
+        for (int k = 0; k < 3; ++k) {
+            a[k] = p[3 + k] - p[k];
+            b[k] = p[6 + k] - p[k];
+        }
+        h[0] = (float)((double)a[1] * b[2] - (double)a[2] * b[1]);
+        h[1] = (float)((double)a[2] * b[0] - (double)a[0] * b[2]);
+        h[2] = (float)((double)a[0] * b[1] - (double)a[1] * b[0]);
+        const double hn = sqrt((double)h[0] * h[0] + (double)h[1] * h[1] + (double)h[2] * h[2]);
+        for (int k = 0; k < 3; ++k) T.n[k] = hn > 0.00001 ? (float)((double)h[k] * (1 / hn)) : h[k];
+        for (int k = 0; k < 3; ++k) {
+            T.p0[k] = p[k];
+            T.v0[k] = a[k];
+            T.v1[k] = b[k];
+        }
+        T.delta = (double)T.n[0] * p[0] + (double)T.n[1] * p[1] + (double)T.n[2] * p[2];
+        T.d00 = (double)a[0] * a[0] + (double)a[1] * a[1] + (double)a[2] * a[2];
+        T.d11 = (double)b[0] * b[0] + (double)b[1] * b[1] + (double)b[2] * b[2];
+        T.d01 = (double)a[0] * b[0] + (double)a[1] * b[1] + (double)a[2] * b[2];
+        T.denom = T.d00 * T.d11 - T.d01 * T.d01;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double t = jsrt::tri_intersect(T, o, d);
+        exact[i] = (t > minD && t < maxD) ? 1 : 0;
+        double e = 0;
+        dec[i] = jsrt::tri_any_f32(T, o, d, minD, maxD, e);
+        tf[i] = e;
+    }
+}

@@ -211,3 +211,54 @@ def test_sphere_any_decisions_are_exact(lib, seed, maxD):
     assert (tf[acc] > 1e-4).all() and (tf[acc] < maxD).all()
     assert ex.sum() > 1000 and (ex == 0).sum() > 1000
     assert (dec[~boundary] == -1).mean() < 1e-3, (dec[~boundary] == -1).mean()
+
+
+def _tri_cases(seed, n=400_000):
+    """Random triangles (mesh-like sizes and slivers) and rays aimed at barycentric points inside, on the
+    edges and vertices, and outside, with segments ending before, at and beyond the triangle."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-3, 3, (n, 1, 3))
+    size = np.exp(rng.uniform(np.log(1e-3), np.log(2), (n, 1, 1)))
+    v = c + rng.normal(size=(n, 3, 3)) * size
+    sliver = rng.random(n) < 0.1
+    v[sliver, 2] = v[sliver, 0] + (v[sliver, 1] - v[sliver, 0]) * rng.uniform(0, 1, (sliver.sum(), 1)) + \
+        rng.normal(scale=1e-4, size=(sliver.sum(), 3)) * size[sliver, 0]
+    bary = rng.dirichlet([1, 1, 1], n)
+    kind = rng.integers(0, 4, n)
+    m = kind == 1  # on an edge
+    e = rng.integers(0, 3, n)
+    bary[m, e[m]] = 0
+    bary[m] /= bary[m].sum(1, keepdims=True)
+    m = kind == 2  # outside
+    bary[m] = bary[m] * 2 - 0.3
+    m = kind == 3  # a vertex
+    bary[m] = np.eye(3)[e[m]]
+    target = (bary[:, :, None] * v).sum(1)
+    o = target + rng.normal(size=(n, 3)) * rng.uniform(0.1, 10, (n, 1))
+    frac = rng.choice([0.3, 0.9, 1.0, 1.1, 3.0, 1e-4], n)
+    d = (target - o) / frac[:, None]
+    verts = v.reshape(n, 9).astype(np.float32)
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    boundary = (kind == 1) | (kind == 3) | (frac == 1.0) | (frac == 1e-4) | sliver
+    return verts, rays, boundary
+
+
+@pytest.mark.parametrize("maxD", [1.0, np.inf])
+@pytest.mark.parametrize("seed", [8, 9])
+def test_tri_any_decisions_are_exact(lib, seed, maxD):
+    import ctypes as C
+    L = lib
+    L.tri_any.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_double, C.c_double, C.c_void_p, C.c_void_p,
+                          C.c_void_p]
+    verts, rays, boundary = _tri_cases(seed)
+    n = len(rays)
+    ex, dec, tf = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n)
+    L.tri_any(verts.ctypes.data, rays.ctypes.data, n, 1e-4, maxD, ex.ctypes.data, dec.ctypes.data, tf.ctypes.data)
+    taken = dec >= 0
+    bad = np.flatnonzero(taken & (dec != ex))
+    assert len(bad) == 0, bad[:8]
+    acc = dec == 1
+    assert (tf[acc] > 1e-4).all() and (tf[acc] < maxD).all()
+    assert ex.sum() > 1000 and (ex == 0).sum() > 1000
+    # (rays up to 30 units long against triangles down to 1e-3: the hit point bound is relative to the ray)
+    assert (dec[~boundary] == -1).mean() < 0.1, (dec[~boundary] == -1).mean()
