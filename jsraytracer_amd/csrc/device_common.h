@@ -188,8 +188,18 @@ __device__ __forceinline__ void sin_cos(double x, double &s, double &c) { fdlibm
 // rest (|value| below ~2^-20, or within 2^-44 of an f32 rounding boundary: about one pick in 10^5) are
 // recomputed with fdlibm, out of line.
 constexpr double SPHERE_PICK_EPS = 0x1p-44;
-__device__ __forceinline__ bool f32_stable(double d) {
-    return (float)(d - SPHERE_PICK_EPS) == (float)(d + SPHERE_PICK_EPS);
+// Whether every value within SPHERE_PICK_EPS of d rounds to d's f32, on the bits of d (|d| <= 2; integer
+// operations, no f64 temporaries; tests/test_box_any.py::test_f32_stable_bits): the f32
+// rounding of d is decided by its low 29 fraction bits against the midpoint 2^28, and 2^-44 is 2^(8 - e)
+// units of d's last place for d in [2^e, 2^(e+1)).  Stable iff the distance to the midpoint exceeds that
+// (|d| < 2^-20: never, the margin reaches half an f32 unit).
+JSRT_HD bool f32_stable_bits(double d) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, d);
+    const int e = (int)((uint32_t)(b >> 52) & 0x7FFu) - 1023;
+    const int sh = 8 - e;
+    const uint32_t m = (uint32_t)b & 0x1FFFFFFFu;
+    const uint32_t dist = m > 0x10000000u ? m - 0x10000000u : 0x10000000u - m;
+    return sh <= 28 && dist > (1u << (sh < 0 ? 0 : sh));
 }
 struct SinCos2 {
     double st, ct, sp, cp;
@@ -210,12 +220,40 @@ __device__ __forceinline__ F3 sphere_pick(R &rng) {
 #else
     sincos(theta, &sin_t, &cos_t);
     sincos(::acos(a), &sin_phi, &cos_phi);
-    const bool fast = f32_stable(cos_t * sin_phi) && f32_stable(cos_phi) && f32_stable(sin_t * sin_phi);
+    const bool fast = f32_stable_bits(cos_t * sin_phi) && f32_stable_bits(cos_phi) && f32_stable_bits(sin_t * sin_phi);
 #endif
     if (__builtin_expect(!fast, 0)) {  // out of line: the hot path keeps OCML's register footprint
         const SinCos2 r = sphere_pick_exact(theta, a);
         sin_t = r.st, cos_t = r.ct, sin_phi = r.sp, cos_phi = r.cp;
     }
+    return f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
+}
+// spherePick for a caller that finishes the unstable picks itself (k_shade, at its tail, where the registers
+// are free: the fallback inline in the scatter cost k_shade ~50 spilled VGPRs and 25 % of its time):
+// OCML's values, with `unstable` set when a product's f32 rounding is not decided within SPHERE_PICK_EPS;
+// sphere_pick_v8 then gives the reference's point from the same two draws.
+template <class R>
+__device__ __forceinline__ F3 sphere_pick_fast(R &rng, bool &unstable) {
+    const double theta = 2.0 * JS_PI * rng.next();
+    const double a = 2.0 * rng.next() - 1.0;
+    double sin_t, cos_t, sin_phi, cos_phi;
+    sincos(theta, &sin_t, &cos_t);
+    sincos(::acos(a), &sin_phi, &cos_phi);
+    const double px = cos_t * sin_phi, pz = sin_t * sin_phi;
+#ifdef JSRT_EXACT_TRIG
+    unstable = true;
+#else
+    unstable = !(f32_stable_bits(px) && f32_stable_bits(cos_phi) && f32_stable_bits(pz));
+#endif
+    return f3((float)px, or0((float)cos_phi), or0((float)pz));
+}
+template <class R>
+__device__ __forceinline__ F3 sphere_pick_v8(R &rng) {
+    const double theta = 2.0 * JS_PI * rng.next();
+    const double a = 2.0 * rng.next() - 1.0;
+    double sin_t, cos_t, sin_phi, cos_phi;
+    fdlibm::sin_cos(theta, sin_t, cos_t);
+    fdlibm::sin_cos(fdlibm::acos(a), sin_phi, cos_phi);
     return f3((float)(cos_t * sin_phi), or0((float)cos_phi), or0((float)(sin_t * sin_phi)));
 }
 // Vec.cartesianToSpherical (math.js:189-193)
@@ -477,8 +515,10 @@ JSRT_HD int tri_any_f32(const DTri &T, F3 o, F3 d, double minD, double maxD, dou
     return -1;
 }
 // a Triangle's distance as a shadow cast reads it (tri_any_f32, the exact test only when too close to call)
+// (opt-in, -DJSRT_TRI_ANY: it raises the mesh k_shadow's spills from 42 to 95 and loses -- bunny k_shadow
+// 26.3 -> 37.2 ms, the dragon 789 -> 749 M/s, profiles/r04_s10_ab.txt)
 JSRT_HD double tri_any(const DTri &T, F3 o, F3 d, double minD, double maxD) {
-#if !defined(JSRT_NO_ANY_FILTER) && !defined(JSRT_NO_TRI_ANY)  // (-DJSRT_NO_TRI_ANY: A/B of the triangle filter)
+#if !defined(JSRT_NO_ANY_FILTER) && defined(JSRT_TRI_ANY)
     double t = 0;
     const int dec = tri_any_f32(T, o, d, minD, maxD, t);
     if (dec >= 0) return dec ? t : -DINF;
@@ -1532,8 +1572,11 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
 }
 
 // PhongPathTracingMaterial.scatter (materials.js:398-412)
+// fix (out): 0, or 1 + the RNG call index of the diffuse pick's first draw when the pick was unstable
+// (sphere_pick_fast): the caller recomputes the direction with sphere_pick_v8 before it is cast
 __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 R, F3 N, const ShadeData &d, Rng &rng,
-                                             F3 &dir, F3 &col) {
+                                             F3 &dir, F3 &col, uint32_t &fix) {
+    fix = 0;
     if (rng.next() < mirror_prob) {
         dir = R;
         col = f3(1, 1, 1);
@@ -1543,7 +1586,10 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
     const double probSum = dp + sp;
     if (probSum == 0) return false;
     if (rng.next() < (dp / probSum)) {  // scatterDiffuse: N.plus(Vec.spherePick().to4()).normalized()
-        const F3 sp3 = sphere_pick(rng);
+        const uint32_t call = rng.calls;
+        bool unstable;
+        const F3 sp3 = sphere_pick_fast(rng, unstable);
+        if (unstable) fix = call + 1;
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;

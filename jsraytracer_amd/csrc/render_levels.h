@@ -255,6 +255,7 @@ struct Handoff {
 struct NodeOut {
     F3 surf;        // surface colour: the final colour of an unlit node, the ambient term of a lit one
     uint32_t info;  // INFO_* bits + child count
+
     Handoff h;      // h.pos (the hit point) is set for every hit; the rest for lit nodes
 };
 
@@ -426,9 +427,14 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
 // World.color hit branch up to the shadow casts: Primitive.color (world.js:125-137) +
 // Geometry.materialData + Material.color (materials.js).  Fills the node (info, ambient / surface,
 // shadow hand-off of its light samples) and returns its children (0..2) in evaluation order.
+// A child whose diffuse direction came from an unstable spherePick (path_scatter's fix) sets INFO_FIX (never
+// stored) and leaves in LDS, in column threadIdx.x of `fixl` [5][256]: fix0, fix1 (1 + the pick's RNG call,
+// bit 31 = scattered about -N, the refraction side; 0 = none) and the node's N.  k_shade recomputes those
+// directions at its tail (fix_child_dirs), so nothing of it is live in registers through the stores.
+constexpr uint32_t INFO_FIX = 1u << 30;
 template <int PF>
 __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
-                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1) {
+                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1, uint32_t *fixl) {
     const DPrim &P = S.prims[h.prim];
     Surface sf;
     surface_data<PF, false>(S, h, o, d, (S.mat_flags[P.material] & MATF_UV) != 0, sf);
@@ -528,6 +534,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         rng.calls = (uint32_t)S.light_draws;
     }
     int n = 0;
+    uint32_t fix0 = 0u, fix1 = 0u;
     auto push = [&](const Child &c) {  // unconditional selects keep both slots in registers
         const bool first = n == 0;
         ch0 = pick(first, c, ch0);
@@ -541,15 +548,35 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
         if (sd.kr > 0) {
             F3 dir = sd.R, col = f3(1, 1, 1);
             bool ok = true;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col);
-            if (ok) push(Child{dir, col, sd.refl, sd.kr});
+            uint32_t fx = 0;
+            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col, fx);
+            if (ok) {
+                fix0 = fx;  // the first child
+                push(Child{dir, col, sd.refl, sd.kr});
+            }
         }
         if (sd.kr < 1) {
             F3 dir = sd.refr, col = f3(1, 1, 1);
             bool ok = sd.has_refr;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col);
-            if (ok) push(Child{dir, col, sd.trans, 1 - sd.kr});
+            uint32_t fx = 0;
+            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col, fx);
+            if (ok) {
+                if (fx) {  // child n (0 when the reflection side pushed none)
+                    if (n == 0) fix0 = fx | 0x80000000u;
+                    else fix1 = fx | 0x80000000u;
+                }
+                push(Child{dir, col, sd.trans, 1 - sd.kr});
+            }
         }
+    }
+    if (__builtin_expect((fix0 | fix1) != 0u, 0)) {
+        const uint32_t t = threadIdx.x;
+        fixl[t] = fix0;
+        fixl[256 + t] = fix1;
+        fixl[512 + t] = __float_as_uint(Nn.x);
+        fixl[768 + t] = __float_as_uint(Nn.y);
+        fixl[1024 + t] = __float_as_uint(Nn.z);
+        info |= INFO_FIX;
     }
     out.info = info | ((uint32_t)n << INFO_NCHILD_SHIFT);
     return n;
@@ -722,6 +749,27 @@ __global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L);
 // World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
 // Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
 // Tree schedule: node = pool slot; children are appended to level L + 1 (block-aggregated).
+// The child directions of unstable spherePicks (NodeOut::fix), recomputed with V8's sin / cos / acos from the
+// pick's own draws and stored over the OCML direction k_shade wrote to ray slot dst[j]: at the kernel's tail,
+// after every other store, so the rare fdlibm evaluation does not raise k_shade's register peak.
+__device__ __attribute__((noinline)) void fix_child_dirs(const WArgs &W, const uint32_t *fixl, uint32_t key, uint32_t addr,
+                                               int nchild, uint32_t d0, uint32_t d1) {
+    const uint32_t t = threadIdx.x;
+    const F3 N = f3(u2f(fixl[512 + t]), u2f(fixl[768 + t]), u2f(fixl[1024 + t]));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t f = fixl[256 * j + t];
+        if (j >= nchild || f == 0u) continue;
+        Rng rg{key, addr, (f & 0x7FFFFFFFu) - 1u};
+        const F3 sp3 = sphere_pick_v8(rg);
+        const F3 dir = normalized(add((f >> 31) ? neg(N) : N, sp3));
+        const uint32_t dst = j == 0 ? d0 : d1;
+        W.dx[dst] = dir.x;
+        W.dy[dst] = dir.y;
+        W.dz[dst] = dir.z;
+    }
+}
+
 template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
     DScene S, WArgs W, int L, int child_depth) {
@@ -741,6 +789,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     int nchild = 0;
     Child ch0, ch1;
     NodeOut out;
+    __shared__ uint32_t fixl[5 * 256];  // shade_node's unstable spherePicks (INFO_FIX)
     const int prim = in ? W.prim[r] : NO_RAY;
     const bool hit = prim >= 0;
     // Every load, and the children's append (a returning atomic), is issued before the node's first
@@ -754,7 +803,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     if (hit) {
         const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
         const Hit h{W.t[r], prim, W.ctx[r]};
-        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1);
+        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1, fixl);
         out.h.node = CHAIN ? slot : q;  // (k_shadow: node base + this)
         out.h.mask = (uint32_t)S.grid_cells;  // every root
         if (W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
@@ -814,7 +863,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     }
     if (nchild > 0 && unit_child(ch0)) out.info |= INFO_UNIT0;
     if (nchild > 1 && unit_child(ch1)) out.info |= INFO_UNIT1;
-    store_node(W, i, out.surf, out.info);
+    store_node(W, i, out.surf, out.info & ~INFO_FIX);
     if (out.info & INFO_LIT) {
         if (!W.bucket) store_hand(W, q, out.h);
         else if (hslot != ~0u) store_hand(W, hslot, out.h);
@@ -845,6 +894,8 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
             W.parent[c] = i;
             W.prim[c] = -1;
         }
+        if (__builtin_expect((out.info & INFO_FIX) != 0u, 0) && child_depth > 0)
+            fix_child_dirs(W, fixl, out.h.key, out.h.addr, W.hybrid ? nchild : 1, r, side_at);
         return;
     }
     if (nchild == 0) return;
@@ -869,6 +920,8 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         W.parent[rr] = 2 * i + (uint32_t)j;
         W.prim[rr] = -1;
     }
+    if (__builtin_expect((out.info & INFO_FIX) != 0u, 0))
+        fix_child_dirs(W, fixl, out.h.key, out.h.addr, nchild, next_base + at + co[0], next_base + at + co[1]);
 }
 
 // The light samples of the lit nodes of level L (lights.js sampleIterator), their shadow casts

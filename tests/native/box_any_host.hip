@@ -78,3 +78,8 @@ extern "C" void tri_any(const float *verts, const float *rays, long n, double mi
         tf[i] = e;
     }
 }
+
+// the spherePick stability test on the bits (device_common.h f32_stable_bits): out[i] = 1 if stable
+extern "C" void stable_bits(const double *d, long n, int *out) {
+    for (long i = 0; i < n; ++i) out[i] = jsrt::f32_stable_bits(d[i]) ? 1 : 0;
+}

@@ -262,3 +262,28 @@ def test_tri_any_decisions_are_exact(lib, seed, maxD):
     assert ex.sum() > 1000 and (ex == 0).sum() > 1000
     # (rays up to 30 units long against triangles down to 1e-3: the hit point bound is relative to the ray)
     assert (dec[~boundary] == -1).mean() < 0.1, (dec[~boundary] == -1).mean()
+
+
+def test_f32_stable_bits(lib):
+    """spherePick's stability test (device_common.h f32_stable_bits): a value it calls stable rounds to the same
+    f32 as every value within 2^-44 of it (checked at the interval's ends and at random points of it), and it
+    calls stable nearly every value the float rounding would (the exact interval test)."""
+    import ctypes as C
+    lib.stable_bits.argtypes = [C.c_void_p, C.c_long, C.c_void_p]
+    rng = np.random.default_rng(11)
+    n = 2_000_000
+    d = rng.uniform(-1, 1, n) * np.exp2(-rng.integers(0, 24, n).astype(np.float64))
+    mid = rng.random(n) < 0.3  # put some within a few 2^-44 of an f32 midpoint
+    f = d[mid].astype(np.float32).astype(np.float64)
+    up = np.nextafter(d[mid].astype(np.float32), np.float32(np.inf)).astype(np.float64)
+    d[mid] = (f + up) / 2 + rng.normal(scale=2.0 ** -44, size=mid.sum()) * rng.choice([0.5, 1, 2, 8], mid.sum())
+    out = np.empty(n, np.int32)
+    lib.stable_bits(np.ascontiguousarray(d).ctypes.data, n, out.ctypes.data)
+    e = 2.0 ** -44
+    ref = (d - e).astype(np.float32) == (d + e).astype(np.float32)
+    st = out == 1
+    for delta in (-e, e, rng.uniform(-e, e, n)):
+        assert ((d + delta).astype(np.float32)[st] == d.astype(np.float32)[st]).all()
+    assert not (st & ~ref).any()
+    assert (ref & ~st).mean() < 1e-4
+    assert st.sum() > n // 2
