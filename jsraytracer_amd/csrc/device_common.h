@@ -204,7 +204,7 @@ JSRT_HD bool f32_stable_bits(double d) {
 struct SinCos2 {
     double st, ct, sp, cp;
 };
-__device__ __attribute__((noinline)) inline SinCos2 sphere_pick_exact(double theta, double a) {
+__device__ __forceinline__ SinCos2 sphere_pick_exact(double theta, double a) {
     SinCos2 r;
     fdlibm::sin_cos(theta, r.st, r.ct);
     fdlibm::sin_cos(fdlibm::acos(a), r.sp, r.cp);
@@ -1575,7 +1575,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
 // fix (out): 0, or 1 + the RNG call index of the diffuse pick's first draw when the pick was unstable
 // (sphere_pick_fast): the caller recomputes the direction with sphere_pick_v8 before it is cast
 __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 R, F3 N, const ShadeData &d, Rng &rng,
-                                             F3 &dir, F3 &col, uint32_t &fix) {
+                                             F3 &dir, F3 &col, uint32_t &fix, bool force) {
     fix = 0;
     if (rng.next() < mirror_prob) {
         dir = R;
@@ -1589,7 +1589,7 @@ __device__ __forceinline__ bool path_scatter(double mirror_prob, bool has_r, F3 
         const uint32_t call = rng.calls;
         bool unstable;
         const F3 sp3 = sphere_pick_fast(rng, unstable);
-        if (unstable) fix = call + 1;
+        if (unstable || force) fix = call + 1;
         dir = normalized(add(N, sp3));
         col = scale(d.diff, 1 / JS_PI);
         return true;

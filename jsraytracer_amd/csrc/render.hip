@@ -219,6 +219,31 @@ __global__ __launch_bounds__(256) void k_resolve_side(RenderArgs A, WArgs W, int
 }
 
 // hybrid chain: every path's colour -> root (k_accum adds them per pixel in sample order)
+__global__ __launch_bounds__(256) void k_fix_dirs(WArgs W) {
+    const uint32_t n = *W.fixctr, m = n < W.fixcap ? n : W.fixcap;
+    // a child slot past the ray arrays belongs to a frame k_shade flagged for a redo (out of chain slots or
+    // pool): not written
+    const size_t bound = W.chain ? (size_t)W.cap : (size_t)W.pool;
+    for (uint32_t k = threadIdx.x; k < m; k += 256) {
+        const uint4 a = W.fixrec[3 * (size_t)k], b = W.fixrec[3 * (size_t)k + 1], c = W.fixrec[3 * (size_t)k + 2];
+        const F3 N = f3(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z));
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t f = j == 0 ? b.x : b.y;
+            if (j >= (int)b.z || f == 0u) continue;
+            Rng rg{a.z, a.w, (f & 0x7FFFFFFFu) - 1u};  // the pick's draws (path_scatter: theta, then acos's argument)
+            const F3 sp3 = sphere_pick_v8(rg);
+            const F3 dir = normalized(add((f >> 31) ? neg(N) : N, sp3));  // scatterDiffuse about N or -N
+            const uint32_t dst = j == 0 ? a.x : a.y;
+            if (dst >= bound) continue;
+            W.dx[dst] = dir.x;
+            W.dy[dst] = dir.y;
+            W.dz[dst] = dir.z;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *W.fixctr = 0u;  // the next level's records
+}
+
 __global__ __launch_bounds__(256) void k_resolve_paths(RenderArgs A, WArgs W) {
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;
     if (q >= W.npaths || W.lvl[LVL_FLAG]) return;
@@ -291,6 +316,11 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree || hybrid) bytes += need(3 * paths, 4);                 // root
     bytes += need(HAND_PLANES * hands, 16) + need(hands, 4) + need(64, 4);  // hand-off + nodes + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
+    // unstable spherePicks per level: ~1e-5 of the nodes (k_fix_dirs); every node under JSRT_FORCE_EXACT_PICK
+    const char *fx = getenv("JSRT_FORCE_EXACT_PICK");
+    const bool force_fix = fx && fx[0] == '1';
+    const size_t fixcap = force_fix ? rays + 4096 : rays / 8 + 4096;
+    bytes += need(3 * fixcap, 16) + need(64, 4);
     if (tree || hybrid)  // buckets
         bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);
     if (mem && bytes <= cap_bytes) {  // carve the cached allocation again
@@ -325,6 +355,10 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     w.hnode = carve<uint32_t>(p, hands);
     w.lvl = carve<uint32_t>(p, 64);
     w.qctr = carve<uint32_t>(p, 64);
+    w.fixrec = carve<uint4>(p, 3 * fixcap);
+    w.fixctr = carve<uint32_t>(p, 64);
+    w.fixcap = (uint32_t)fixcap;
+    w.force_fix = force_fix ? 1 : 0;
     if (shadow) { w.sray = carve<float4>(p, 2 * shadow); w.scol = carve<float4>(p, shadow); }
     if (tree || hybrid) {
         w.bkt = carve<uint32_t>(p, MAX_TREE_DEPTH * BKT_LEVEL);
@@ -668,9 +702,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             W2.hand = t.hand; W2.hnode = t.hnode; W2.root = t.root; W2.lvl = t.lvl; W2.qctr = t.qctr; W2.sray = t.sray;
             W2.scol = t.scol; W2.bkt = t.bkt; W2.bbase = t.bbase; W2.brank = t.brank;
             W2.list0 = t.list0; W2.list1 = t.list1; W2.endl = t.endl;
+            W2.fixrec = t.fixrec; W2.fixctr = t.fixctr; W2.fixcap = t.fixcap;
         }
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
         if (learned && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
+        if ((e = hipMemsetAsync(W.fixctr, 0, sizeof(uint32_t), st)) != hipSuccess) break;
+        if (dual && (e = hipMemsetAsync(W2.fixctr, 0, sizeof(uint32_t), st)) != hipSuccess) break;
         if (dual) {  // the side stream starts after everything enqueued on st so far
             if ((e = hipEventRecord(ev_start, st)) != hipSuccess || (e = hipStreamWaitEvent(st2, ev_start, 0)) != hipSuccess) break;
             if (learned && (e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;

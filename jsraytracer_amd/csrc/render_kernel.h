@@ -76,6 +76,12 @@ struct WArgs {
     // persistent casts (SDF scenes, render.hip k_extend_q / k_shadow_*): work counters per level
     // ([L] extend, [32 + L] shadow) and the shadow rays of the light samples ([e] = k_shadow lane e)
     uint32_t *qctr;
+    // child directions of unstable spherePicks (k_shade's INFO_FIX), recomputed by k_fix_dirs before the next
+    // level's casts: fixctr[0] records of 3 x uint4 {dst0, dst1, key, addr} {fix0, fix1, nchild, -} {N, -}
+    uint4 *fixrec;
+    uint32_t *fixctr;
+    uint32_t fixcap;
+    int32_t force_fix;  // JSRT_FORCE_EXACT_PICK=1 (tests): every diffuse pick through k_fix_dirs
     float4 *sray;      // [e] {P.xyz, -}, [sstride + e] {delta.xyz, -}
     float4 *scol;      // [e] {unshadowed colour.xyz, state: 0 no cast / lit, 1 cast pending, 2 shadowed}
     // hit-primitive buckets of the lit nodes per level (W.bucket), BKT_LEVEL words from L * BKT_LEVEL:

@@ -434,7 +434,8 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
 constexpr uint32_t INFO_FIX = 1u << 30;
 template <int PF>
 __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &h, F3 o, F3 d, uint32_t addr,
-                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1, uint32_t *fixl) {
+                                          uint32_t key, NodeOut &out, Child &ch0, Child &ch1, uint32_t *fixl,
+                                          bool force_fix) {
     const DPrim &P = S.prims[h.prim];
     Surface sf;
     surface_data<PF, false>(S, h, o, d, (S.mat_flags[P.material] & MATF_UV) != 0, sf);
@@ -549,7 +550,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
             F3 dir = sd.R, col = f3(1, 1, 1);
             bool ok = true;
             uint32_t fx = 0;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col, fx);
+            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, true, sd.R, Nn, sd, rng, dir, col, fx, force_fix);
             if (ok) {
                 fix0 = fx;  // the first child
                 push(Child{dir, col, sd.refl, sd.kr});
@@ -559,7 +560,7 @@ __device__ __forceinline__ int shade_node(const DScene &S, bool lit, const Hit &
             F3 dir = sd.refr, col = f3(1, 1, 1);
             bool ok = sd.has_refr;
             uint32_t fx = 0;
-            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col, fx);
+            if (mkind == JSRT_MAT_PATH) ok = path_scatter(M.mirror_prob, sd.has_refr, sd.refr, neg(Nn), sd, rng, dir, col, fx, force_fix);
             if (ok) {
                 if (fx) {  // child n (0 when the reflection side pushed none)
                     if (n == 0) fix0 = fx | 0x80000000u;
@@ -749,26 +750,28 @@ __global__ __launch_bounds__(256) void k_bucket_offsets(WArgs W, int L);
 // World.color at level L (world.js:31-41): a miss is bg_color, a hit is shaded (shade_node).
 // Chain schedule (every node has <= 1 child): node L*P + q, its child ray replaces ray q.
 // Tree schedule: node = pool slot; children are appended to level L + 1 (block-aggregated).
-// The child directions of unstable spherePicks (NodeOut::fix), recomputed with V8's sin / cos / acos from the
-// pick's own draws and stored over the OCML direction k_shade wrote to ray slot dst[j]: at the kernel's tail,
-// after every other store, so the rare fdlibm evaluation does not raise k_shade's register peak.
-__device__ __attribute__((noinline)) void fix_child_dirs(const WArgs &W, const uint32_t *fixl, uint32_t key, uint32_t addr,
-                                               int nchild, uint32_t d0, uint32_t d1) {
+// A node with unstable spherePicks (INFO_FIX): its record for k_fix_dirs (rare: about one pick in 10^5), with
+// the ray slots its children's directions went to.  Out of records (never: fixcap is 1/8 of the level's
+// slots), the frame is redone with a larger pool, as for any other capacity.
+__device__ __forceinline__ void fix_record(const WArgs &W, const uint32_t *fixl, uint32_t key, uint32_t addr,
+                                           int nchild, uint32_t d0, uint32_t d1) {
     const uint32_t t = threadIdx.x;
-    const F3 N = f3(u2f(fixl[512 + t]), u2f(fixl[768 + t]), u2f(fixl[1024 + t]));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const uint32_t f = fixl[256 * j + t];
-        if (j >= nchild || f == 0u) continue;
-        Rng rg{key, addr, (f & 0x7FFFFFFFu) - 1u};
-        const F3 sp3 = sphere_pick_v8(rg);
-        const F3 dir = normalized(add((f >> 31) ? neg(N) : N, sp3));
-        const uint32_t dst = j == 0 ? d0 : d1;
-        W.dx[dst] = dir.x;
-        W.dy[dst] = dir.y;
-        W.dz[dst] = dir.z;
+    const uint32_t k = atomicAdd(W.fixctr, 1u);
+    if (k >= W.fixcap) {
+        W.lvl[LVL_FLAG] = 1u;
+        return;
     }
+    uint4 *r = W.fixrec + 3 * (size_t)k;
+    r[0] = make_uint4(d0, d1, key, addr);
+    r[1] = make_uint4(fixl[t], fixl[256 + t], (uint32_t)nchild, 0u);
+    r[2] = make_uint4(fixl[512 + t], fixl[768 + t], fixl[1024 + t], 0u);
 }
+
+// The child directions of the level's unstable spherePicks, recomputed with V8's sin / cos / acos (fdlibm.h)
+// from each pick's own draws and stored over the OCML direction k_shade wrote: a separate one-block kernel
+// after k_shade, so the fdlibm code is not part of k_shade (inline there it cost ~50 spilled VGPRs, as a call
+// a 416-B stack frame per lane; either slowed k_shade 25 % to 4x, profiles/r04_s10_ab.txt, r04_s11_ab.txt).
+__global__ __launch_bounds__(256) void k_fix_dirs(WArgs W);
 
 template <int PF, bool CHAIN>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
@@ -803,7 +806,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     if (hit) {
         const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
         const Hit h{W.t[r], prim, W.ctx[r]};
-        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1, fixl);
+        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1, fixl, W.force_fix != 0);
         out.h.node = CHAIN ? slot : q;  // (k_shadow: node base + this)
         out.h.mask = (uint32_t)S.grid_cells;  // every root
         if (W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
@@ -835,6 +838,12 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         const int side = (child_depth > 0 && nchild > 1) ? 1 : 0, cont = (child_depth > 0 && nchild > 0) ? 1 : 0;
         block_append2(W.lvl + 2 * (L + 1), cont, side, at, side_at);
         side_at += side_base(W, L + 1);
+    }
+    // unstable spherePicks: the record for k_fix_dirs, with the slots the children's rays go to below (written
+    // before the node's stores, behind which the returning atomic would wait for all of them)
+    if (__builtin_expect(hit && (out.info & INFO_FIX) != 0u, 0) && child_depth > 0) {
+        if (CHAIN) fix_record(W, fixl, out.h.key, out.h.addr, W.hybrid ? nchild : 1, r, side_at);
+        else fix_record(W, fixl, out.h.key, out.h.addr, nchild, next_base + at + co[0], next_base + at + co[1]);
     }
     // ---- stores ----
     if (prim == NO_RAY) {
@@ -894,8 +903,6 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
             W.parent[c] = i;
             W.prim[c] = -1;
         }
-        if (__builtin_expect((out.info & INFO_FIX) != 0u, 0) && child_depth > 0)
-            fix_child_dirs(W, fixl, out.h.key, out.h.addr, W.hybrid ? nchild : 1, r, side_at);
         return;
     }
     if (nchild == 0) return;
@@ -920,8 +927,6 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         W.parent[rr] = 2 * i + (uint32_t)j;
         W.prim[rr] = -1;
     }
-    if (__builtin_expect((out.info & INFO_FIX) != 0u, 0))
-        fix_child_dirs(W, fixl, out.h.key, out.h.addr, nchild, next_base + at + co[0], next_base + at + co[1]);
 }
 
 // The light samples of the lit nodes of level L (lights.js sampleIterator), their shadow casts
@@ -1256,6 +1261,7 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         if (split && L > 0 && W.ns > 0) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the hand-off is free
         timed(KT_SHADE, [&] {
             hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
+            if (child_depth > 0) hipLaunchKernelGGL(k_fix_dirs, dim3(1), dim3(256), 0, st, W);
         });
         if (W.ns > 0 && split) {
             (void)hipEventRecord(sync->shade_done, st);

@@ -106,6 +106,24 @@ def test_gpu_frame_redo_paths(jr, monkeypatch):
         assert np.array_equal(a, b) and np.array_equal(ca.view(np.uint32), cb.view(np.uint32))
 
 
+@pytest.mark.parametrize("name,W,H,spp,seed", [("cornell_box_path", 48, 48, 4, 13), ("refraction_path", 40, 40, 4, 3),
+                                               ("bunny", 48, 40, 2, 5)])
+def test_gpu_exact_pick_fixup_path(jr, monkeypatch, name, W, H, spp, seed):
+    """Every diffuse spherePick through k_fix_dirs (JSRT_FORCE_EXACT_PICK=1: each pick treated as unstable, its
+    direction recomputed with fdlibm by the one-block kernel after k_shade), in the hybrid chain (cornell), the
+    tree with two children per hit (refraction_path) and a mesh (bunny): the frame must equal the oracle's and
+    the default path's bit for bit.  (Unforced, about one pick in 10^5 takes this path.)"""
+    blob = pyoracle.golden_scene(name)
+    depth = pyoracle.scene_header(blob)["max_depth"]
+    ref = jr.Scene(blob, device=0).render(W, H, spp, depth, 1, seed)
+    monkeypatch.setenv("JSRT_FORCE_EXACT_PICK", "1")
+    got = jr.Scene(blob, device=0).render(W, H, spp, depth, 1, seed)
+    monkeypatch.delenv("JSRT_FORCE_EXACT_PICK")
+    ocol, orgba, _ = pyoracle.render(blob, W, H, spp, depth, 1, seed)
+    _compare(got[0], got[1], orgba, ocol, f"{name} forced exact picks")
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1].view(np.uint32), got[1].view(np.uint32))
+
+
 def test_gpu_progress_callback(jr):
     """renderers.js:103-112: callback({pass, completion}) while rendering, completion increasing."""
     sc = _scene(jr, "cornell_box_path")
