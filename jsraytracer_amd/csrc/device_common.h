@@ -1393,6 +1393,9 @@ __device__ __forceinline__ void march_step(const DScene &S, MarchState &m, doubl
 // The persistent loop.  Src: bool load(uint32_t job, F3 &o, F3 &d) (false: no ray in that slot),
 // void store(uint32_t job, const Hit &h).  Jobs [0, count) are taken from *ctr.  FO: every SDF root
 // of the scene is a recognised form (sdf_form_dist), no stack VM.
+#ifndef JSRT_MARCH_STEPS
+#define JSRT_MARCH_STEPS 4
+#endif
 template <int PF, bool ANY, bool FO, class Src>
 __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, uint32_t count, double minD,
                                                 double maxD, bool transp, Src &src) {
@@ -1430,7 +1433,16 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
                 have = false;
             }
         }
-        if (have && m.marching) march_step<ANY, FO>(S, m, minD, maxD);
+        // up to JSRT_MARCH_STEPS march steps per refill round: the refill (ballot, atomic, ray loads) and the
+        // root walk of the lanes that finished run once per round instead of once per step, at the price of
+        // a finished lane idling for the rest of its round
+        if (__any(have && m.marching)) {
+#pragma unroll 1
+            for (int k = 0; k < JSRT_MARCH_STEPS; ++k) {
+                if (have && m.marching) march_step<ANY, FO>(S, m, minD, maxD);
+                if (!__any(have && m.marching)) break;
+            }
+        }
     }
 }
 
@@ -1524,7 +1536,9 @@ __device__ __forceinline__ F3 light_sample_color(int mkind, const ShadeData &d, 
 // One sample of lights.js sampleIterator for `Lt` seen from world point P: the direction (delta, NOT
 // normalised: the shadow ray's t in (1e-4, 1) spans the segment) and the sample colour.
 // LT: DLight in any address space (a wave-uniform record is read through the constant one: scalar loads)
-template <class LT, class RNG>
+// SPH: the scene may have a sphere area light (DScene::sphere_lights); without one the spherePick and its
+// fdlibm fallback are not compiled into the caller (k_shadow: never executed, they cost it 5 ms on cornell)
+template <bool SPH = true, class LT, class RNG>
 __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P, RNG &rng, F3 &delta, F3 &L,
                                              F3 &lcol) {
     if (Lt.kind == JSRT_LIGHT_POINT) {  // SimplePointLight.sampleIterator (lights.js:45-53)
@@ -1535,7 +1549,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
         lcol = scale(mc_eval(S, Lt.color, u, v), 1 / (4 * JS_PI * dot3(delta, delta)));
     } else {  // RandomSampleAreaLight.sampleIterator (lights.js:80-92)
         F3 local;
-        if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Vec.spherePick().to4(1)
+        if (SPH && Lt.gkind == JSRT_GEOM_SPHERE) {  // Vec.spherePick().to4(1)
             local = sphere_pick(rng);
         } else {  // Square / Circle.sampleSurface (geometry.js:295-300, 326-331)
             const double a = rng.next() - 0.5;
@@ -1549,7 +1563,7 @@ __device__ __forceinline__ void light_sample(const DScene &S, const LT &Lt, F3 P
         delta = sub(wpos, P);
         F3 wn;
         float u, v;
-        if (Lt.gkind == JSRT_GEOM_SPHERE) {  // Sphere.materialData: local.normalized() (w = 1 term included)
+        if (SPH && Lt.gkind == JSRT_GEOM_SPHERE) {  // Sphere.materialData: local.normalized() (w = 1 term included)
             const double nn = sqrt(dot3(local, local) + 1.0);
             F3 n = local;
             float nw = 1.0f;

@@ -158,7 +158,7 @@ struct DScene {
     const DTri *ltris;       // parallel to leaf_prims: the triangle of a fast leaf entry (leaf order)
     const int32_t *prim_lit; // per prim: 1 if its material takes light samples (not Solid / Transparent)
     int32_t sdf_all_forms;   // every SDF geometry root is a recognised program form (sdf_forms.h)
-    int32_t pad_forms;
+    int32_t sphere_lights;   // an area light samples a Sphere (spherePick in k_shadow; its kernel variant)
     // Spatial buckets of the shadow hand-off (scene_load.cpp shadow_grid): hit points binned on a grid of
     // grid_cells <= 63 cells over the bounded top-level objects (bucket grid_cells: outside the grid), and
     // per bucket the top-level objects a shadow segment from that cell to any light can meet

@@ -942,16 +942,16 @@ __device__ __forceinline__ F3 mc_const3(const DScene &S, int m) {  // a constant
     const float4 c = *reinterpret_cast<const float4 *>(S.mc_const + 4 * m);
     return f3(c.x, c.y, c.z);
 }
-template <int PF>
+template <int PF, bool SPH = true>
 __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
     const float4 h0 = hp[0], h1 = hp[hs];
     P = f3(h0.x, h0.y, h0.z);
     RngH rng{f2u(h0.w), (uint32_t)S.sample_call[s]};
     F3 L, lcol;
     if (S.n_lights == 1)  // (kernel argument: uniform) the light record through scalar loads
-        light_sample(S, as_const(S.lights)[0], P, rng, delta, L, lcol);
+        light_sample<SPH>(S, as_const(S.lights)[0], P, rng, delta, L, lcol);
     else
-        light_sample(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
+        light_sample<SPH>(S, S.lights[S.sample_light[s]], P, rng, delta, L, lcol);
     const uint32_t tag = f2u(h1.w);
     const jsrt_rec_material &M = S.mat[(tag & HAND_MAT) >> 8];
     ShadeData sd;
@@ -976,11 +976,11 @@ __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *h
 
 __device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
 
-template <int PF>
+template <int PF, bool SPH = true>
 __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s,
                                            uint64_t mask = ~0ull) {
     F3 P, delta;
-    const F3 c = sample_unshadowed<PF>(S, hp, hs, s, P, delta);
+    const F3 c = sample_unshadowed<PF, SPH>(S, hp, hs, s, P, delta);
     // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
@@ -1009,7 +1009,7 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
     return ret;
 }
 
-template <int PF, bool CHAIN, bool SERIAL>
+template <int PF, bool CHAIN, bool SERIAL, bool SPH>
 __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DScene S, WArgs W, int L) {
     const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
     const uint32_t count = R.count, base = R.base;
@@ -1049,14 +1049,14 @@ __global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DSc
             const DLight &Lt = S.lights[li];
             const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
             F3 light_color = f3(0, 0, 0);
-            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF>(S, hp, W.hstride, k, mask));
+            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF, SPH>(S, hp, W.hstride, k, mask));
             if (n > 0) ret = add(ret, scale(light_color, Lt.inv_n));  // times(1 / samples)
         }
         W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
         return;
     }
     F3 c = f3(0, 0, 0);
-    if (lit && s < ns) c = sample_color<PF>(S, hp, W.hstride, s, mask);
+    if (lit && s < ns) c = sample_color<PF, SPH>(S, hp, W.hstride, s, mask);
     ret = light_sums(S, G, ret, c);
     if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
@@ -1280,10 +1280,16 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                         hipLaunchKernelGGL((k_shadow_cast<PF, CHAIN, false>),
                                            dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN, false>, ne)), dim3(256), 0, st, S, W, L);
                     hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
-                } else if (W.ns <= 1 || W.group > 1)
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
-                else
-                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
+                } else if (W.ns <= 1 || W.group > 1) {
+                    if (S.sphere_lights)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
+                    else
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
+                } else if (S.sphere_lights) {
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
+                } else {
+                    hipLaunchKernelGGL((k_shadow<PF, CHAIN, true, false>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
+                }
             });
         if (W.ns > 0 && split) (void)hipEventRecord(sync->shadow_done, ss);
     }
