@@ -1394,10 +1394,10 @@ __device__ __forceinline__ void march_step(const DScene &S, MarchState &m, doubl
 // void store(uint32_t job, const Hit &h).  Jobs [0, count) are taken from *ctr.  FO: every SDF root
 // of the scene is a recognised form (sdf_form_dist), no stack VM.
 #ifndef JSRT_MARCH_STEPS
-#define JSRT_MARCH_STEPS 2
+#define JSRT_MARCH_STEPS 8
 #endif
 #ifndef JSRT_MARCH_KEEP
-#define JSRT_MARCH_KEEP 0
+#define JSRT_MARCH_KEEP 56
 #endif
 template <int PF, bool ANY, bool FO, class Src>
 __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, uint32_t count, double minD,
@@ -1439,7 +1439,8 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
         // up to JSRT_MARCH_STEPS march steps per refill round while at least JSRT_MARCH_KEEP lanes still march:
         // the refill (ballot, atomic, ray loads) and the root walk of the lanes that finished run once per
         // round instead of once per step, at the price of a finished lane idling for the rest of its round
-        // (SDF_Menger: 1 step 118.8 M/s, 2 steps 150.7, 4 steps 127.6, 8 steps 99.1; profiles/r04_s13_ab.txt)
+        // (SDF_Menger: 1 step 118.8 M/s, 2 steps 150.7 / 147.6, 4 steps 127.6, 8 steps 99.1; up to 8 steps while
+        // >= 56 lanes march 151.7, >= 48 149.4; profiles/r04_s13_ab.txt, r04_s14_ab.txt)
         if (__any(have && m.marching)) {
 #pragma unroll 1
             for (int k = 0; k < JSRT_MARCH_STEPS; ++k) {

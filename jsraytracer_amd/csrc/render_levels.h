@@ -784,8 +784,43 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     } else if (tt >= count) {
         return;
     }
+#ifdef JSRT_SHADE_SORT
+    // (A/B) the block's nodes permuted by hit primitive through LDS (a counting sort on min(prim, 62), misses
+    // and idle lanes last), so a wave shades nodes of one or two primitives: one geometry branch, one material
+    __shared__ uint32_t s_cnt[64], s_perm[256];
+    uint32_t tq = tt;
+    if (!CHAIN || W.hybrid) {  // (kernel argument: block-uniform; the plain chain returns per thread above)
+        uint32_t key = 63u;
+        if (tt < count) {
+            const uint32_t s0 = CHAIN ? chain_slot(W, L, tt) : tt;
+            const int p0 = W.prim[CHAIN ? s0 : base + tt];
+            key = p0 >= 0 ? (uint32_t)(p0 < 62 ? p0 : 62) : 63u;
+        }
+        if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        const uint32_t rank = atomicAdd(&s_cnt[key], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 64 counts in one wave
+            const uint32_t c = s_cnt[threadIdx.x];
+            uint32_t x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if ((int)threadIdx.x >= o) x += y;
+            }
+            s_cnt[threadIdx.x] = x - c;
+        }
+        __syncthreads();
+        s_perm[s_cnt[key] + rank] = threadIdx.x;
+        __syncthreads();
+        tq = t0 + s_perm[threadIdx.x];
+    }
+    const bool in = tq < count;
+    const uint32_t q = in ? tq : 0u;                          // level index
+#else
     const bool in = tt < count;
     const uint32_t q = in ? tt : 0u;                          // level index
+#endif
     const uint32_t slot = CHAIN && in ? chain_slot(W, L, q) : q;  // chain: the chain's slot
     const uint32_t i = base + (CHAIN ? slot : q);             // node index (chain: L * cap + slot)
     const uint32_t r = CHAIN ? slot : i;                      // ray index
