@@ -635,12 +635,7 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
     const CONST_AS double *K = as_const(S.sdf_const);
     pc = uni(pc);  // uniform among the active lanes (sdf_node_dist's waterfall)
     end = uni(end);
-    if (uni(code[pc].op) == SOP_FORM) {  // a recognised shape: straight-line code (sdf_forms.h)
-        const int form = uni(code[pc].a);
-        if (form == SFORM_RUNION_DIFF) return sdf_form_runion_diff(K, code, pc + 1, P);
-        if (form == SFORM_RUNION) return sdf_form_runion(K, code, pc + 1, P);
-        ++pc;  // (unknown form: the VM runs its instructions)
-    }
+    if (uni(code[pc].op) == SOP_FORM) return sdf_form_any(K, code, pc, P);  // straight-line code (sdf_forms.h)
     while (pc < end) {
         const int op = uni(code[pc].op), ia = uni(code[pc].a), ib = uni(code[pc].b);
         switch (op) {
@@ -772,8 +767,7 @@ __device__ __forceinline__ double sdf_form_dist(const DScene &S, int n, F3 p) {
     for (;;) {  // waterfall over the lanes' nodes (a wave marches one SDF in every reference scene)
         const int pcu = uni(pc);
         if (pc == pcu) {
-            const int form = uni(code[pcu].a);
-            r = form == SFORM_RUNION_DIFF ? sdf_form_runion_diff(K, code, pcu + 1, p) : sdf_form_runion(K, code, pcu + 1, p);
+            r = sdf_form_any(K, code, pcu, p);
             break;
         }
     }

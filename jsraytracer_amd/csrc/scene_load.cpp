@@ -636,13 +636,55 @@ struct Loader {
             for (int32_t i = 0; ok && i < 10; ++i) ok = I[at + i].op == runion[i];
             return ok && I[at + 3].b == begin + at + 7 && I[at + 7].a == begin + at + 3;  // LOOP brackets [4, 6]
         };
-        int32_t form = 0;
+        auto is_prim = [&](int32_t at) {
+            return at < n && (I[at].op == SOP_BOX || I[at].op == SOP_SPHERE || I[at].op == SOP_TETRA);
+        };
+        // TransformSDF(primitive, Matrix) at [at, at + 7): PUSHP TPUSH XMAT PRIM MULS TPOP POPP
+        auto is_tprim = [&](int32_t at) {
+            return at + 7 <= n && I[at].op == SOP_PUSHP && I[at + 1].op == SOP_TPUSH && I[at + 2].op == SOP_XMAT &&
+                   is_prim(at + 3) && I[at + 4].op == SOP_MULS && I[at + 5].op == SOP_TPOP && I[at + 6].op == SOP_POPP;
+        };
+        int32_t form = 0, fflags = 0, fpad = 0;
         if (n == 10 && is_runion(0)) form = SFORM_RUNION;
         else if (n == 13 && I[0].op == SOP_BOX && is_runion(1) && I[11].op == SOP_NEG && I[12].op == SOP_MAX && I[12].a == 2)
             form = SFORM_RUNION_DIFF;
+        else if (is_tprim(0)) {  // SFORM_PAIR: tprim [NEG] tprim [NEG] (MIN 2 | MAX 2 | SMIN) [NEG]
+            int32_t j = 7, fl = 0;
+            if (j < n && I[j].op == SOP_NEG) { fl |= SPAIR_NEG_A; ++j; }
+            const int32_t ob = j;
+            if (is_tprim(j)) {
+                j += 7;
+                if (j < n && I[j].op == SOP_NEG) { fl |= SPAIR_NEG_B; ++j; }
+                bool comb = true;
+                if (j < n && I[j].op == SOP_MIN && I[j].a == 2) {
+                } else if (j < n && I[j].op == SOP_MAX && I[j].a == 2) {
+                    fl |= SPAIR_MAX;
+                } else if (j < n && I[j].op == SOP_SMIN) {
+                    fl |= SPAIR_SMIN;
+                } else {
+                    comb = false;
+                }
+                if (comb) {
+                    ++j;
+                    if (j < n && I[j].op == SOP_NEG) { fl |= SPAIR_NEG_OUT; ++j; }
+                    if (j == n) { form = SFORM_PAIR; fflags = fl; fpad = ob; }
+                }
+            }
+        } else if (n >= 11 && I[0].op == SOP_PUSHP && I[1].op == SOP_TPUSH && I[2].op == SOP_LOOP &&
+                   I[3].op == SOP_TPUSH && I[4].op == SOP_XMATS) {  // SFORM_TXREC
+            int32_t m = 0;
+            while (5 + m < n && I[5 + m].op == SOP_XREF) ++m;
+            const int32_t e = 6 + m;  // ENDLOOP
+            if (n == 11 + m && I[5 + m].op == SOP_TPOP_MUL && I[e].op == SOP_ENDLOOP && I[2].b == begin + e &&
+                I[e].a == begin + 2 && is_prim(7 + m) && I[8 + m].op == SOP_MULS && I[9 + m].op == SOP_TPOP &&
+                I[10 + m].op == SOP_POPP) {
+                form = SFORM_TXREC;
+                fflags = m;
+            }
+        }
         if (!form) return {begin, end};
         const int32_t fb = (int32_t)S.sdf_insn.size();
-        S.sdf_insn.push_back(SdfInsn{SOP_FORM, form, 0, 0});
+        S.sdf_insn.push_back(SdfInsn{SOP_FORM, form, fflags, fpad});
         for (int32_t i = 0; i < n; ++i) {
             SdfInsn c = S.sdf_insn[begin + i];
             if (c.op == SOP_LOOP) c.b += fb + 1 - begin;

@@ -46,3 +46,81 @@ __device__ __forceinline__ double sdf_form_runion_diff(const KT *K, const CT *co
     const double d1 = sdf_form_runion(K, code, pc + 1, P);
     return js_max(d0, -d1);
 }
+
+// One primitive of a form: BOX / SPHERE / TETRA at instruction `pc` (the VM's cases, sdf.js:232-234,
+// 276-279, 305-308), the opcode read uniform.
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_prim(const KT *K, const CT *code, int pc, F3 P) {
+    const int op = uni(code[pc].op), ia = uni(code[pc].a);
+    if (op == SOP_BOX) return sdf_box(K + ia, P);
+    if (op == SOP_SPHERE) {
+        const F3 q = f3(P.x, or0(P.y), or0(P.z));
+        return sqrt(dot3(q, q)) - K[ia];
+    }
+    return (js_max(fabs((double)P.x + (double)P.y) - (double)P.z, fabs((double)P.x - (double)P.y) + (double)P.z) - 1) /
+           sqrt(3.0);
+}
+
+// SFORM_PAIR: TransformSDF(primitive, Matrix) twice, combined (sdf.js:83-85, 99-101, 117-119, 128-131,
+// 330-333; SDF_Combinations).  Each operand is [0] PUSHP [1] TPUSH [2] XMAT a b [3] PRIM [4] MULS [5] TPOP
+// [6] POPP: prim(M P) * (1 * k); the flags say which of the operands and the result the program negates
+// and which combiner follows (MIN 2, MAX 2 or SMIN k at pc + cb).  The VM's operations in its order.
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_tprim(const KT *K, const CT *code, int pc, F3 P) {
+    const int xa = uni(code[pc + 2].a), xb = uni(code[pc + 2].b);
+    return sdf_form_prim(K, code, pc + 3, xf_point(K + xa, P)) * (1.0 * K[xb]);
+}
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_pair(const KT *K, const CT *code, int pc, int flags, int off_b, F3 P) {
+    double a = sdf_form_tprim(K, code, pc, P);
+    if (flags & SPAIR_NEG_A) a = -a;
+    double b = sdf_form_tprim(K, code, pc + off_b, P);
+    if (flags & SPAIR_NEG_B) b = -b;
+    const int cb = off_b + 7 + ((flags & SPAIR_NEG_B) ? 1 : 0);
+    double r;
+    if (flags & SPAIR_SMIN) {  // smoothMin (sdf.js:128-131)
+        const double k = K[uni(code[pc + cb].a)];
+        const double h = js_max(k - fabs(a - b), 0.0) / k;
+        r = js_min(a, b) - h * h * h * k * (1.0 / 6.0);
+    } else {
+        r = (flags & SPAIR_MAX) ? js_max(a, b) : js_min(a, b);
+    }
+    return (flags & SPAIR_NEG_OUT) ? -r : r;
+}
+
+// SFORM_TXREC: TransformSDF(primitive, SDFRecursiveTransformer(Sequence(Matrix, Reflection x m), n)) --
+// SDF_Sierpinski (tests/SDF_Sierpinski/test.mjs: a tetrahedron folded 10 times by a scaling and three
+// reflections).  Program: [0] PUSHP [1] TPUSH [2] LOOP n [3] TPUSH [4] XMATS a b [5 .. 5+m) XREF [5+m]
+// TPOP_MUL [6+m] ENDLOOP [7+m] PRIM [8+m] MULS [9+m] TPOP [10+m] POPP.  Per iteration P = M P, then each
+// reflection (sdf.js:450-455: P - n * 2 (n.P - delta) when n.P - delta < 0), the iteration's scale
+// 1 * (1 * k) multiplied into the outer one; the result prim(P) * scale.
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_txrec(const KT *K, const CT *code, int pc, int m, F3 P) {
+    const int iters = uni(code[pc + 2].a);
+    const int xa = uni(code[pc + 4].a), xb = uni(code[pc + 4].b);
+    double s0 = 1.0;
+    F3 Q = P;
+    for (int it = 0; it < iters; ++it) {
+        double s1 = 1.0;
+        Q = xf_point(K + xa, Q);
+        s1 = s1 * (1.0 * K[xb]);
+        for (int j = 0; j < m; ++j) {
+            const int ra = uni(code[pc + 5 + j].a);
+            const F3 n = f3((float)K[ra], (float)K[ra + 1], (float)K[ra + 2]);
+            const double dt = dot3(n, Q) - K[ra + 3];
+            if (dt < 0) Q = sub(Q, scale(n, 2 * dt));
+        }
+        s0 = s0 * s1;
+    }
+    return sdf_form_prim(K, code, pc + 7 + m, Q) * s0;
+}
+
+// Any recognised form at the marker pc (uniform): its straight-line code
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_any(const KT *K, const CT *code, int pc, F3 P) {
+    const int form = uni(code[pc].a);
+    if (form == SFORM_RUNION_DIFF) return sdf_form_runion_diff(K, code, pc + 1, P);
+    if (form == SFORM_RUNION) return sdf_form_runion(K, code, pc + 1, P);
+    if (form == SFORM_PAIR) return sdf_form_pair(K, code, pc + 1, uni(code[pc].b), uni(code[pc].pad), P);
+    return sdf_form_txrec(K, code, pc + 1, uni(code[pc].b), P);
+}
