@@ -258,8 +258,8 @@ __device__ __forceinline__ F3 sphere_pick_v8(R &rng) {
 }
 // Vec.cartesianToSpherical (math.js:189-193)
 __device__ __forceinline__ void cart_to_sph(F3 n, float &u, float &v) {
-    u = (float)(0.5 + atan2((double)n.z, (double)n.x) / (2 * JS_PI));
-    v = (float)(0.5 - asin((double)n.y) / JS_PI);
+    u = (float)(0.5 + fdlibm::atan2((double)n.z, (double)n.x) / (2 * JS_PI));  // V8's atan2 / asin (fdlibm.h)
+    v = (float)(0.5 - fdlibm::asin((double)n.y) / JS_PI);
 }
 
 // --------------------------------------------------------------------------------------------

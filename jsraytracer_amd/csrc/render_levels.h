@@ -329,7 +329,7 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
     case JSRT_GEOM_CYLINDER:  // geometry.js:479-487
         nrm = normalized(f3(pl.x, pl.y, 0));
         if (need_uv) {
-            u = (float)(0.5 + atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
+            u = (float)(0.5 + fdlibm::atan2((double)pl.y, (double)pl.x) / (2 * JS_PI));
             v = (float)(0.5 + (double)pl.z);
         }
         has_uv = 1;

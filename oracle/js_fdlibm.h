@@ -4,7 +4,10 @@
  * (v8/src/base/ieee754.cc: __kernel_sin, __kernel_cos, __ieee754_rem_pio2, __ieee754_acos); the C
  * library's sin / cos / acos differ from those in the last float64 bit on ~3 % of arguments.  Pinned bit
  * for bit to node's results on 3.3 M arguments (tests/golden/trig_v8.npz, tests/test_oracle_trig.py).
- * Arguments beyond 2^19 pi/2 (none on the render path) fall back to the C library.
+ * Arguments beyond 2^19 pi/2 (none on the render path) fall back to the C library.  Math.atan2 and Math.asin
+ * (Vec.cartesianToSpherical, math.js:189-193, and the cylinder UV, geometry.js:479-487) likewise: fdlibm's
+ * atan / __ieee754_atan2 / __ieee754_asin, pinned to node on 4 M argument pairs (tests/golden/uv_v8.npz);
+ * the C library differs from them on 18 % / 6 % of unit-vector arguments.
  */
 #ifndef JS_FDLIBM_H
 #define JS_FDLIBM_H
@@ -155,4 +158,132 @@ static double js_acos(double x) { /* __ieee754_acos */
     w = r * s + c;
     return 2.0 * (df + w);
 }
+static double fd_atan(double x) { /* atan (s_atan.c) */
+    static const double atanhi[] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01, 1.57079632679489655800e+00};
+    static const double atanlo[] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17, 6.12323399573676603587e-17};
+    static const double aT[] = {3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                                -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                                -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+    double w, s1, s2, z;
+    int32_t ix, hx, id;
+    hx = (int32_t)fd_hi(x);
+    ix = hx & 0x7fffffff;
+    if (ix >= 0x44100000) {
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && (fd_lo(x) != 0))) return x + x;
+        if (hx > 0) return atanhi[3] + atanlo[3];
+        else return -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3fdc0000) {
+        if (ix < 0x3e200000) return x;
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else {
+            if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+            else { id = 3; x = -1.0 / x; }
+        }
+    }
+    z = x * x;
+    w = z * z;
+    s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (hx < 0) ? -z : z;
+}
+static double js_atan2(double y, double x) { /* __ieee754_atan2 (FreeBSD msun form, as V8) */
+    const double tiny = 1.0e-300, zero = 0.0, pi_o_4 = 7.8539816339744827900E-01, pi_o_2 = 1.5707963267948965580E+00,
+                 pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    double z;
+    int32_t k, m, hx, hy, ix, iy;
+    uint32_t lx, ly;
+    hx = (int32_t)fd_hi(x); ix = hx & 0x7fffffff; lx = fd_lo(x);
+    hy = (int32_t)fd_hi(y); iy = hy & 0x7fffffff; ly = fd_lo(y);
+    if (((uint32_t)ix | ((lx | -lx) >> 31)) > 0x7ff00000u || ((uint32_t)iy | ((ly | -ly) >> 31)) > 0x7ff00000u) return x + y;
+    if (((hx - 0x3ff00000) | (int32_t)lx) == 0) return fd_atan(y);
+    m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if ((iy | ly) == 0) {
+        switch (m) {
+        case 0: case 1: return y;
+        case 2: return pi + tiny;
+        case 3: return -pi - tiny;
+        }
+    }
+    if ((ix | lx) == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7ff00000) {
+        if (iy == 0x7ff00000) {
+            switch (m) {
+            case 0: return pi_o_4 + tiny;
+            case 1: return -pi_o_4 - tiny;
+            case 2: return 3.0 * pi_o_4 + tiny;
+            case 3: return -3.0 * pi_o_4 - tiny;
+            }
+        } else {
+            switch (m) {
+            case 0: return zero;
+            case 1: return -zero;
+            case 2: return pi + tiny;
+            case 3: return -pi - tiny;
+            }
+        }
+    }
+    if (iy == 0x7ff00000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    k = (iy - ix) >> 20;
+    if (k > 60) { z = pi_o_2 + 0.5 * pi_lo; m &= 1; }
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = fd_atan(fabs(y / x));
+    switch (m) {
+    case 0: return z;
+    case 1: return -z;
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}
+static double js_asin(double x) { /* __ieee754_asin */
+    const double one = 1.0, huge = 1.0e300, pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17,
+                 pio4_hi = 7.85398163397448278999e-01, pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
+                 pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02, pS4 = 7.91534994289814532176e-04,
+                 pS5 = 3.47933107596021167570e-05, qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
+                 qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+    double t = 0, w, p, q, c, r, s;
+    int32_t hx, ix;
+    hx = (int32_t)fd_hi(x);
+    ix = hx & 0x7fffffff;
+    if (ix >= 0x3ff00000) {
+        if (((ix - 0x3ff00000) | (int32_t)fd_lo(x)) == 0) return x * pio2_hi + x * pio2_lo;
+        return (x - x) / (x - x);
+    } else if (ix < 0x3fe00000) {
+        if (ix < 0x3e400000) {
+            if (huge + x > one) return x;
+        } else {
+            t = x * x;
+        }
+        p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+        q = one + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+        w = p / q;
+        return x + x * w;
+    }
+    w = one - fabs(x);
+    t = w * 0.5;
+    p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+    q = one + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+    s = sqrt(t);
+    if (ix >= 0x3FEF3333) {
+        w = p / q;
+        t = pio2_hi - (2.0 * (s + s * w) - pio2_lo);
+    } else {
+        w = fd_words(fd_hi(s), 0);
+        c = (t - w * w) / (s + w);
+        r = p / q;
+        p = 2.0 * s * r - (pio2_lo - 2.0 * c);
+        q = pio4_hi - 2.0 * w;
+        t = pio4_hi - (p - q);
+    }
+    return hx > 0 ? t : -t;
+}
+
 #endif

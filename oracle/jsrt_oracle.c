@@ -309,7 +309,7 @@ static Vec ray_point(Ray r, double t) { return vplus(r.o, vtimes(r.d, t)); } /* 
 
 /* cartesianToSpherical (math.js:189-193) */
 static Vec cart_to_sph(Vec n) {
-    return vof2(0.5 + atan2(n.v[2], n.v[0]) / (2 * JS_PI), 0.5 - asin(n.v[1]) / JS_PI);
+    return vof2(0.5 + js_atan2(n.v[2], n.v[0]) / (2 * JS_PI), 0.5 - js_asin(n.v[1]) / JS_PI);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -1093,7 +1093,7 @@ static int material_data(Ctx *C, int o, Ray ray, double distance, const Mat *anc
     case JSRT_GEOM_CYLINDER: /* geometry.js:479-487 */
         d.has_normal = d.has_uv = 1;
         d.normal = vnormalized(vof4(pos.v[0], pos.v[1], 0, 0));
-        d.uv = vof2(0.5 + atan2(pos.v[1], pos.v[0]) / (2 * JS_PI), 0.5 + (double)pos.v[2]);
+        d.uv = vof2(0.5 + js_atan2(pos.v[1], pos.v[0]) / (2 * JS_PI), 0.5 + (double)pos.v[2]);
         break;
     case JSRT_GEOM_AABB: { /* geometry.js:210-224 */
         double norm_dist = 0;
@@ -1428,6 +1428,13 @@ int jsrt_oracle_sdf_distance(const void *blob, size_t blob_bytes, int32_t obj, c
 }
 
 /* Math.sin / Math.cos / Math.acos of n arguments (tests/test_oracle_trig.py: pinned to node's results) */
+void jsrt_oracle_uv(const double *xy, double *out, long n) {
+    for (long i = 0; i < n; ++i) {
+        out[2 * i] = js_atan2(xy[2 * i + 1], xy[2 * i]);
+        out[2 * i + 1] = js_asin(xy[2 * i]);
+    }
+}
+
 void jsrt_oracle_trig(const double *x, double *out, long n) {
     for (long i = 0; i < n; ++i) {
         out[3 * i] = js_sin(x[i]);

@@ -21,3 +21,10 @@ extern "C" int npio2_hw_ok(void) {
         if (jsrt::fdlibm::hi_word((double)n * 1.57079632679489655800e+00) != tab[n - 1]) return 0;
     return 1;
 }
+
+extern "C" void uv_n(const double *xy, double *out, long n) {  // per (x, y): atan2(y, x), asin(x)
+    for (long i = 0; i < n; ++i) {
+        out[2 * i] = jsrt::fdlibm::atan2(xy[2 * i + 1], xy[2 * i]);
+        out[2 * i + 1] = jsrt::fdlibm::asin(xy[2 * i]);
+    }
+}

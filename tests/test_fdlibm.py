@@ -14,7 +14,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "native", "fdlibm_host.hip")
 OUT = os.path.join(ROOT, "tests", "native", "_build", "libfdlibm_host.so")
-HDR = os.path.join(ROOT, "jsraytracer_amd", "csrc", "fdlibm.h")
+HDR = os.path.join(ROOT, "jsraytracer_amd", "csrc", "fdlibm.h")  # (rebuilt when it changes)
 
 
 @pytest.fixture(scope="module")
@@ -62,3 +62,30 @@ def test_fdlibm_matches_v8_everywhere(lib):
 def test_reduction_table_computed(lib):
     """fdlibm.h computes rem_pio2's npio2_hw table (high words of n pi/2) instead of indexing it per lane."""
     assert lib.npio2_hw_ok() == 1
+
+
+def _uv(L, xy):
+    import ctypes as C
+    L.uv_n.argtypes = [C.c_void_p, C.c_void_p, C.c_long]
+    xy = np.ascontiguousarray(xy, dtype=np.float64)
+    y = np.empty((len(xy), 2))
+    L.uv_n(xy.ctypes.data, y.ctypes.data, len(xy))
+    return y
+
+
+def test_fdlibm_atan2_asin_match_v8(lib):
+    """Math.atan2 / Math.asin (fdlibm.h) against node on 4 M pairs (tests/golden/uv_v8.npz): f32 unit-vector
+    components as cartesianToSpherical takes them, cylinder points, wide pairs, signed zeros, infinities, NaN."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "refharness"))
+    from regen_trig_kats import digest
+    from regen_uv_kats import uv_args
+    g = np.load(os.path.join(ROOT, "tests", "golden", "uv_v8.npz"))
+    sub = _uv(lib, g["sub_xy"])
+    for k, name in enumerate(("atan2", "asin")):
+        ok = _same(sub[:, k], g["sub_y"][:, k])
+        assert ok.all(), f"{name}: {int((~ok).sum())} differ, e.g. {g['sub_xy'][~ok][:4].tolist()}"
+    xy = uv_args(int(g["args_seed"][0]))
+    assert len(xy) == int(g["n"][0])
+    y = _uv(lib, xy)
+    for k, name in enumerate(("atan2", "asin")):
+        assert digest(y[:, k]) == str(g[f"sha_{name}"]), name

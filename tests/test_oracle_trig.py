@@ -31,3 +31,19 @@ def test_oracle_trig_matches_v8():
     y = _trig(trig_args(int(g["args_seed"][0])))
     for k, name in enumerate(("sin", "cos", "acos")):
         assert digest(y[:, k]) == str(g[f"sha_{name}"]), name
+
+
+def test_oracle_atan2_asin_match_v8():
+    """The oracle's Math.atan2 / Math.asin (oracle/js_fdlibm.h) against node on 4 M pairs (tests/golden/uv_v8.npz)."""
+    from oracle import pyoracle
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "refharness"))
+    from regen_trig_kats import digest
+    from regen_uv_kats import uv_args
+    L = pyoracle.lib()
+    L.jsrt_oracle_uv.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+    g = np.load(os.path.join(ROOT, "tests", "golden", "uv_v8.npz"))
+    xy = np.ascontiguousarray(uv_args(int(g["args_seed"][0])))
+    y = np.empty((len(xy), 2))
+    L.jsrt_oracle_uv(xy.ctypes.data, y.ctypes.data, len(xy))
+    for k, name in enumerate(("atan2", "asin")):
+        assert digest(y[:, k]) == str(g[f"sha_{name}"]), name
