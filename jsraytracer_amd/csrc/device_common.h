@@ -54,7 +54,7 @@ JSRT_HD double js_sign(double x) {
     return x > 0 ? 1.0 : -1.0;
 }
 // (ah + al) * (bh + bl) in double-double (Dekker / fma two-product): relative error ~2^-104
-__device__ __forceinline__ void dd_mul(double ah, double al, double bh, double bl, double &rh, double &rl) {
+JSRT_HD void dd_mul(double ah, double al, double bh, double bl, double &rh, double &rl) {
     const double p = ah * bh;
     const double e = fma(ah, bh, -p) + (ah * bl + al * bh);
     rh = p + e;
@@ -64,7 +64,7 @@ __device__ __forceinline__ void dd_mul(double ah, double al, double bh, double b
 // the correctly rounded power except for a value within ~2^-100 relative of a rounding boundary (libm's
 // f64 pow -- V8's fdlibm, glibc, OCML -- is itself only within ~1 ulp there).  A third of the VALU
 // of OCML's general pow for the Phong exponents the reference scenes use (10, 100).
-__device__ __forceinline__ double pow_int_dd(double x, int n) {
+JSRT_HD double pow_int_dd(double x, int n) {
     double bh = x, bl = 0.0, rh = 1.0, rl = 0.0;
     bool first = true;  // the first factor is copied, not multiplied into (1, 0): dd_mul's outputs are
                         // normalised, so 1 x (bh, bl) would return (bh, bl) unchanged
