@@ -645,7 +645,11 @@ struct Loader {
                    is_prim(at + 3) && I[at + 4].op == SOP_MULS && I[at + 5].op == SOP_TPOP && I[at + 6].op == SOP_POPP;
         };
         int32_t form = 0, fflags = 0, fpad = 0;
-        if (n == 10 && is_runion(0)) form = SFORM_RUNION;
+        if (n == 1 && is_prim(0)) form = SFORM_PRIM;
+        else if (n == 7 && I[0].op == SOP_PUSHP && I[1].op == SOP_TPUSH && (I[2].op == SOP_XMAT || I[2].op == SOP_XREP) &&
+                 is_prim(3) && I[4].op == SOP_MULS && I[5].op == SOP_TPOP && I[6].op == SOP_POPP)
+            form = SFORM_TX1;
+        else if (n == 10 && is_runion(0)) form = SFORM_RUNION;
         else if (n == 13 && I[0].op == SOP_BOX && is_runion(1) && I[11].op == SOP_NEG && I[12].op == SOP_MAX && I[12].a == 2)
             form = SFORM_RUNION_DIFF;
         else if (is_tprim(0)) {  // SFORM_PAIR: tprim [NEG] tprim [NEG] (MIN 2 | MAX 2 | SMIN) [NEG]

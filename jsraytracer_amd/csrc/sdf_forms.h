@@ -115,6 +115,15 @@ __device__ __forceinline__ double sdf_form_txrec(const KT *K, const CT *code, in
     return sdf_form_prim(K, code, pc + 7 + m, Q) * s0;
 }
 
+// SFORM_TX1: TransformSDF(primitive, one Matrix or Repetition transformer) (sdf.js:330-333; SDF_SphereRepetition):
+// [0] PUSHP [1] TPUSH [2] XMAT a b | XREP a [3] PRIM [4] MULS [5] TPOP [6] POPP.  XMAT: prim(M P) * (1 * k); XREP
+// (sdf.js:471-473, the scale untouched): prim(rep(P)) * 1.
+template <class KT, class CT>
+__device__ __forceinline__ double sdf_form_tx1(const KT *K, const CT *code, int pc, F3 P) {
+    if (uni(code[pc + 2].op) == SOP_XMAT) return sdf_form_tprim(K, code, pc, P);
+    return sdf_form_prim(K, code, pc + 3, sdf_xrep(K + uni(code[pc + 2].a), P)) * 1.0;
+}
+
 // Any recognised form at the marker pc (uniform): its straight-line code
 template <class KT, class CT>
 __device__ __forceinline__ double sdf_form_any(const KT *K, const CT *code, int pc, F3 P) {
@@ -122,5 +131,7 @@ __device__ __forceinline__ double sdf_form_any(const KT *K, const CT *code, int 
     if (form == SFORM_RUNION_DIFF) return sdf_form_runion_diff(K, code, pc + 1, P);
     if (form == SFORM_RUNION) return sdf_form_runion(K, code, pc + 1, P);
     if (form == SFORM_PAIR) return sdf_form_pair(K, code, pc + 1, uni(code[pc].b), uni(code[pc].pad), P);
-    return sdf_form_txrec(K, code, pc + 1, uni(code[pc].b), P);
+    if (form == SFORM_TXREC) return sdf_form_txrec(K, code, pc + 1, uni(code[pc].b), P);
+    if (form == SFORM_PRIM) return sdf_form_prim(K, code, pc + 1, P);
+    return sdf_form_tx1(K, code, pc + 1, P);
 }

@@ -49,6 +49,8 @@ enum SdfForm : int32_t {
     SFORM_RUNION = 2,       // RecursiveTransformUnion(Union(Box...), Sequence(Matrix, Repetition))
     SFORM_PAIR = 3,         // two Matrix-transformed primitives combined (Union / Intersection / Difference / Smooth*)
     SFORM_TXREC = 4,        // Transform(primitive, Recursive(Sequence(Matrix, Reflection...)))  (SDF_Sierpinski)
+    SFORM_PRIM = 5,         // a bare primitive (SDF_Simple)
+    SFORM_TX1 = 6,          // Transform(primitive, Matrix | Repetition)  (SDF_SphereRepetition)
 };
 // SFORM_PAIR flags (the form instruction's b; its pad = the second operand's offset after the marker)
 enum : int32_t { SPAIR_NEG_A = 1, SPAIR_NEG_B = 2, SPAIR_NEG_OUT = 4, SPAIR_MAX = 8, SPAIR_SMIN = 16 };
