@@ -240,11 +240,7 @@ __device__ __forceinline__ F3 sphere_pick_fast(R &rng, bool &unstable) {
     sincos(theta, &sin_t, &cos_t);
     sincos(::acos(a), &sin_phi, &cos_phi);
     const double px = cos_t * sin_phi, pz = sin_t * sin_phi;
-#ifdef JSRT_EXACT_TRIG
-    unstable = true;
-#else
-    unstable = !(f32_stable_bits(px) && f32_stable_bits(cos_phi) && f32_stable_bits(pz));
-#endif
+    unstable = !(f32_stable_bits(px) && f32_stable_bits(cos_phi) && f32_stable_bits(pz));  // (forced: JSRT_FORCE_EXACT_PICK)
     return f3((float)px, or0((float)cos_phi), or0((float)pz));
 }
 template <class R>
