@@ -27,6 +27,9 @@
 #ifndef JSRT_SHADOW_OCC
 #define JSRT_SHADOW_OCC 6
 #endif
+#ifndef JSRT_SHADOW_OCC_FLAT  // analytic profile: 7 waves (72 VGPRs, no spill) once k_shadow carries no sphere-light code
+#define JSRT_SHADOW_OCC_FLAT 7
+#endif
 #ifndef JSRT_EXTEND_OCC
 #define JSRT_EXTEND_OCC 5
 #endif
@@ -1045,7 +1048,8 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
 }
 
 template <int PF, bool CHAIN, bool SERIAL, bool SPH>
-__global__ __launch_bounds__(256, JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(DScene S, WArgs W, int L) {
+__global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(
+    DScene S, WArgs W, int L) {
     const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
     const uint32_t count = R.count, base = R.base;
     const uint32_t G = (uint32_t)W.group, ns = (uint32_t)W.ns;
