@@ -66,6 +66,9 @@ SIMDS = 256 * 4
 # half the f32 rate 4; transcendentals 4x their type's rate)
 ISSUE_CYC = {"f64": 4.0, "trans_f64": 16.0, "trans_f32": 8.0, "other": 2.0}
 TOL = 1e-5                  # north_star: RGB L-inf on the f32 colour handed to setColor
+# Whether FETCH_SIZE counts 4-B-per-lane coalesced loads at their full bytes on gfx950 (tools/fetch_calib.hip;
+# set from its committed measurement, profiles/fetch_calib_r05.txt)
+FETCH_4B_EXACT = False
 
 
 def env_int(name, default):
@@ -169,7 +172,8 @@ def parity(image, colors, ref):
 
 # environment knobs that change the library's schedule (A/B experiments, tools/ab_env.sh) or swap the library
 # itself (JSRT_LIB: a variant build); JSRT_BENCH_BACKEND only picks the multi-rank gather backend
-NOT_KNOBS = ("JSRT_BENCH_BACKEND",)
+# (JSRT_OFFLOAD_ARCH is a build variable: it never changes a built library's behaviour at run time)
+NOT_KNOBS = ("JSRT_BENCH_BACKEND", "JSRT_OFFLOAD_ARCH")
 
 
 def knobs():
@@ -185,25 +189,47 @@ def exit_status(par):
     return 0
 
 
+def _stage_kernel(kernels, kname, weight):
+    """The stage's kernel among `kernels` (any template instance, or its persistent-cast form k_extend_q)."""
+    hits = [k for k in kernels if k.split("<")[0] in (kname, kname + "_q")]
+    return max(hits, key=lambda h: weight(kernels[h])) if hits else None
+
+
 def load_pmc(config, kname):
-    """Counters of kernel `kname` (any template instance: one kernel profile runs per scene)."""
+    """Counters of kernel `kname` (any template instance: one kernel profile runs per scene), the summary's
+    source and the library build its passes ran (tools/pmc_summary.py)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
-        return None, None, kname
+        return None, None, kname, None
     d = json.load(open(p)).get(config)
     if not d:
-        return None, None, kname
-    # the stage's kernel: any template instance, or its persistent-cast form (k_extend_q: SDF scenes)
-    hits = [k for k in d["kernels"] if k.split("<")[0] in (kname, kname + "_q")]
-    if not hits:
-        return None, None, kname
-    k = max(hits, key=lambda h: d["kernels"][h].get("SQ_WAVE_CYCLES", d["kernels"][h].get("dispatches", 0)))
-    return d["kernels"][k], d.get("source"), k
+        return None, None, kname, None
+    k = _stage_kernel(d["kernels"], kname, lambda c: c.get("SQ_WAVE_CYCLES", c.get("dispatches", 0)))
+    if k is None:
+        return None, None, kname, None
+    return d["kernels"][k], d.get("source"), k, d.get("build_id")
 
 
-def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
+def load_rocprof(config, kname, build_id):
+    """The committed rocprofv3 kernel summary of this build and config (profiles/*_kernel_stats.meta.json,
+    tools/stamp_stats.py): (file, kernel, average launch ms) of the stage's kernel, or None."""
+    import glob
+    for meta in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_kernel_stats.meta.json"))):
+        try:
+            m = json.load(open(meta))
+        except ValueError:
+            continue
+        if m.get("build_id") != build_id or m.get("config") != config:
+            continue
+        k = _stage_kernel(m["kernels"], kname, lambda c: c["calls"] * c["avg_ms"])
+        if k:
+            return os.path.relpath(meta, ROOT), k, m["kernels"][k]["avg_ms"]
+    return None
+
+
+def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame, build_id=None):
     """dom: the dominant kernel; avg_ms: its average launch duration from the HIP events that bracketed
-    its launches in the timed region (on the render stream)."""
+    its launches in the timed region (on the render stream); build_id: the timed library's."""
     per_sample, bpu, unit = kernel_units(counts, dom) if counts else (None, None, None)
     r = {"bound": bound, "kernel": dom, "avg_launch_ms": avg_ms, "launches_per_step": launches,
          "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
@@ -219,11 +245,20 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
                             "units_per_launch": units_per_launch, "GBs": per_launch / sec / 1e9,
                             "frac_of_hbm": per_launch / sec / 1e9 / HBM_PEAK_GBS,
                             "note": "SURVEY.md §8(d) scene-record bytes; > 1 of HBM means cache-served"}
-    pmc, src, r["kernel"] = load_pmc(config, dom)
+    pmc, src, r["kernel"], pmc_bid = load_pmc(config, dom)
+    rp = load_rocprof(config, dom, build_id)
+    if rp:  # the committed rocprofv3 summary of the same build: its average launch time beside the live one
+        r["rocprof"] = {"file": rp[0], "kernel": rp[1], "avg_launch_ms": rp[2], "live_over_rocprof": avg_ms / rp[2]}
     if pmc:
         n = pmc["dispatches"]
-        traffic = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n  # KB -> B, gfx950 x2 on reads
+        # FETCH_SIZE (KB): MI355X_MICROARCH.md reads 1/2 of the bytes of wide (16 B/lane) coalesced streaming
+        # loads on gfx950; other widths are uncalibrated.  This path's loads are mostly 4-B SoA planes, whose
+        # calibration (tools/fetch_calib.hip, profiles/fetch_calib_*.txt) decides which reading is `traffic`.
+        raw = (pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n
+        x2 = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n
+        traffic = raw if FETCH_4B_EXACT else x2
         r["traffic"] = traffic
+        r["traffic_readings"] = {"fetch_x1": raw, "fetch_x2": x2, "used": "fetch_x1" if FETCH_4B_EXACT else "fetch_x2"}
         r["traffic_GBs"] = traffic / sec / 1e9
         r["traffic_frac"] = r["traffic_GBs"] / HBM_PEAK_GBS
         f64 = pmc.get("SQ_INSTS_VALU_ADD_F64", 0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0) + pmc.get("SQ_INSTS_VALU_FMA_F64", 0)
@@ -239,7 +274,10 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame):
                      "valu_insts_per_launch": pmc.get("SQ_INSTS_VALU", 0) / n,
                      "note": "issue_frac: wave64 VALU issue cycles (f64 4, f32/int 2, transcendental 8/16) over "
                              "1024 SIMDs x 2.4 GHz x launch time -- the resource that binds a cache-resident scene"}
-        r["pmc_source"] = src
+        r["pmc_source"] = {"summary": src, "build_id": pmc_bid, "timed_build_id": build_id,
+                           "same_build": pmc_bid is not None and pmc_bid == build_id}
+        if not r["pmc_source"]["same_build"]:  # counters of another build than the one timed: flagged, not hidden
+            r["pmc_build_mismatch"] = True
     if bound == "hbm" and "algorithmic" in r:
         r.update(unit="GB/s", peak=HBM_PEAK_GBS, achieved=r["algorithmic"]["GBs"], frac=r["algorithmic"]["frac_of_hbm"])
         # the BVH and triangles (16 MB for the dragon) are served from L2 / MALL: `frac` counts algorithmic
@@ -400,7 +438,8 @@ def main():
             # the last timed frame (world 1, col_block 1: owned column c is image column c)
             par = parity(timed_image, timed_cols, ref)
             par["frame"] = "last timed step"
-        roof = roofline(args.config, bound, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp)
+        roof = roofline(args.config, bound, dom, dom_ms / max(dom_launches, 1), dom_launches, counts, fg.ncols * H * spp,
+                        jr._native.build_id())
         size = f"{W}²" if W == H else f"{W}x{H}"
         line = {
             "metric": METRIC.format(scene=scene_name, size=size),

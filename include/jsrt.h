@@ -102,6 +102,19 @@ int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col
 int jsrt_render_device_progress(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
                                 float *d_colors, void *hip_stream, jsrt_progress_fn progress, void *user,
                                 jsrt_stats *stats);
+/* (jsrt_render / jsrt_render_device_progress call back on clean passes only: a pass of a batch that outgrew
+ * its device pool or launch bound -- the frame is then redone after its last batch, and passes already
+ * reported are not reported again -- is skipped, so a callback never sees a stale preview.) */
+
+/* The multi-rank form of jsrt_render_device_progress (jsraytracer_amd/tiles.py render_progressive): progress
+ * is called for EVERY pass the frame reports, clean = 1 when the device tile holds that pass's running mean
+ * (0: a batch was poisoned; the tile is not a preview), so every rank calls back the same passes and can keep
+ * its collectives in step (a rank that owns no column still reports each pass).  A non-zero return aborts the
+ * frame: the call returns -4 ("render aborted by the progress callback") once the device is idle. */
+typedef int32_t (*jsrt_progress_ex_fn)(int32_t pass, double completion, int32_t clean, void *user);
+int jsrt_render_device_progress_ex(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
+                                   float *d_colors, void *hip_stream, jsrt_progress_ex_fn progress, void *user,
+                                   jsrt_stats *stats);
 
 /* World.cast(ray, min_dist, max_dist, intersect_transparent) (world.js:28-30) of n rays on the scene's
  * device: rays = n x 6 f32 host array (origin xyz with w = 1, direction xyz with w = 0, as

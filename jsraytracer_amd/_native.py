@@ -44,11 +44,14 @@ class Stats(ctypes.Structure):
 
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)
+# jsrt_progress_ex_fn(pass, completion, clean, user) -> non-zero aborts the frame
+PROGRESS_EX_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_void_p)
+RC_ABORTED = -4  # jsrt_render_device_progress_ex: the callback asked to stop the frame
 
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_cast",
            "jsrt_material_data", "jsrt_sdf_distance", "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version",
-           "jsrt_device_count", "jsrt_build_id", "jsrt_render_device_progress"]
+           "jsrt_device_count", "jsrt_build_id", "jsrt_render_device_progress", "jsrt_render_device_progress_ex"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 # exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
@@ -95,7 +98,10 @@ def lib():
     built = L.jsrt_build_id().decode()
     if not os.environ.get("JSRT_LIB"):  # A/B variants (JSRT_LIB) carry their own defines, hence their own id
         from . import build as _b
-        want = _b.build_id()
+        try:
+            want = _b.build_id()
+        except OSError as e:  # a tree without the sources the id is computed from
+            raise JsrtError(f"cannot verify {LIB_PATH}: its sources are missing ({e})") from e
         if built != want:
             raise JsrtError(f"{LIB_PATH} was built from other sources (build id {built}, this tree {want}): rebuild it")
     L.jsrt_scene_create.restype = ctypes.c_int
@@ -112,6 +118,10 @@ def lib():
     L.jsrt_render_device_progress.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, PROGRESS_FN, ctypes.c_void_p,
                                               ctypes.POINTER(Stats)]
+    L.jsrt_render_device_progress_ex.restype = ctypes.c_int
+    L.jsrt_render_device_progress_ex.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, PROGRESS_EX_FN,
+                                                 ctypes.c_void_p, ctypes.POINTER(Stats)]
     L.jsrt_cast.restype = ctypes.c_int
     L.jsrt_cast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double, ctypes.c_double,
                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]

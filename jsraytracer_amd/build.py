@@ -58,7 +58,10 @@ def build_id(defines=()):
         with open(_path(f), "rb") as fh:
             h.update(fh.read())
         h.update(b"\0")
-    h.update(" ".join(FLAGS + NO_MLICM + [ARCH] + list(defines)).encode())
+    # the flags without the target: a library built with JSRT_OFFLOAD_ARCH set is still the same sources' build
+    # (its code object names its own target), and a run-time environment cannot make a valid library stale
+    flags = [f for f in FLAGS if not f.startswith("--offload-arch=")]
+    h.update(" ".join(flags + NO_MLICM + list(defines)).encode())
     return h.hexdigest()[:16]
 
 

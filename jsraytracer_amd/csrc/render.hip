@@ -316,10 +316,11 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     if (tree || hybrid) bytes += need(3 * paths, 4);                 // root
     bytes += need(HAND_PLANES * hands, 16) + need(hands, 4) + need(64, 4);  // hand-off + nodes + level counts
     bytes += need(64, 4) + need(2 * shadow, 16) + need(shadow, 16);  // work counters + shadow rays
-    // unstable spherePicks per level: ~1e-5 of the nodes (k_fix_dirs); every node under JSRT_FORCE_EXACT_PICK
+    // unstable spherePicks per level: ~1e-5 of the nodes (k_fix_dirs); every node under JSRT_FORCE_EXACT_PICK,
+    // or after a frame that ran out of records (fix_all: the frame is redone with one record per ray slot)
     const char *fx = getenv("JSRT_FORCE_EXACT_PICK");
     const bool force_fix = fx && fx[0] == '1';
-    const size_t fixcap = force_fix ? rays + 4096 : rays / 8 + 4096;
+    const size_t fixcap = (force_fix || fix_all) ? rays + 4096 : rays / 8 + 4096;
     bytes += need(3 * fixcap, 16) + need(64, 4);
     if (tree || hybrid)  // buckets
         bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);
@@ -537,6 +538,16 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                         const std::function<bool()> &due) {
     if (!A.accum) return hipErrorInvalidValue;
     const uint32_t npix_total = (uint32_t)A.patches * 64u;
+    if (npix_total == 0) {  // a rank that owns no column (a multi-GPU frame narrower than its column blocks):
+        // nothing to trace, but an Incremental frame's passes are still reported, so that the rank's callbacks
+        // keep step with its peers' (tiles.render_progressive runs one collective per reported pass)
+        if (progress && A.kind == JSRT_RENDERER_INCREMENTAL) {
+            const uint32_t step = A.samples_per_batch > 0 ? (uint32_t)A.samples_per_batch : (uint32_t)A.spp;
+            for (uint32_t s_end = step; s_end < (uint32_t)A.spp; s_end += step)
+                if ((!due || due()) && !progress((int)s_end - 1, (double)s_end / A.spp, true)) break;
+        }
+        return hipSuccess;
+    }
     if (ns > 4) max_paths = max_paths * 4 / (size_t)ns;  // the per-sample hand-off scales with ns
     if (max_paths < 64) max_paths = 64;
     uint32_t npix = npix_total, nsb = 1;  // batch: [p0, p0 + npix) pixels x [s0, s0 + nsb) samples
@@ -574,14 +585,17 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     const double margin = bm_env ? atof(bm_env) : 1.25;
     const size_t slack = bm_env ? 0 : 4096;
     if (learned && (wf.pool_paths != paths || wf.pool_mode != sched)) {  // learned pool / bounds: per batch shape
-        wf.pool_factor = pf_env ? std::max(1, atoi(pf_env)) : (hybrid ? HYBRID_POOL_FACTOR : 8);
+        // (a batch of at most 1 M paths starts with 3 side-chain slots per path: a band of columns through a
+        // glass sphere outgrows the default 0.5 -- a redo the memory of small batches need not risk)
+        wf.pool_factor = pf_env ? std::max(1, atoi(pf_env))
+                                : (hybrid ? (paths <= ((size_t)1 << 20) ? 8 : HYBRID_POOL_FACTOR) : 8);
         wf.frac.clear();
         wf.pool_paths = paths;
         wf.pool_mode = sched;
     }
     hipError_t e = hipSuccess;
-    uint32_t *h_lvl = nullptr;  // read-back of the level counts and frame flags (tree / hybrid schedule)
-    if (learned && (e = hipHostMalloc((void **)&h_lvl, 128 * sizeof(uint32_t), 0)) != hipSuccess) return e;
+    uint32_t *h_lvl = nullptr;  // read-back of the level counts (tree / hybrid schedule) and the frame flags
+    if ((e = hipHostMalloc((void **)&h_lvl, 128 * sizeof(uint32_t), 0)) != hipSuccess) return e;
     // Two batch pools on two streams: consecutive batches alternate between them, so one batch's levels
     // (latency-bound casts, VALU-bound shadow samples, their launch tails) overlap the other's.  Only the
     // accumulation into A.accum is ordered across them -- each batch's k_accum / k_resolve waits for the
@@ -705,23 +719,21 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             W2.fixrec = t.fixrec; W2.fixctr = t.fixctr; W2.fixcap = t.fixcap;
         }
         if ((e = hipMemsetAsync(A.accum, 0, (size_t)A.ncols * A.H * 4 * sizeof(float), st)) != hipSuccess) break;
-        if (learned && (e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;
+        if ((e = hipMemsetAsync(W.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st)) != hipSuccess) break;  // frame flags
         if ((e = hipMemsetAsync(W.fixctr, 0, sizeof(uint32_t), st)) != hipSuccess) break;
         if (dual && (e = hipMemsetAsync(W2.fixctr, 0, sizeof(uint32_t), st)) != hipSuccess) break;
         if (dual) {  // the side stream starts after everything enqueued on st so far
             if ((e = hipEventRecord(ev_start, st)) != hipSuccess || (e = hipStreamWaitEvent(st2, ev_start, 0)) != hipSuccess) break;
-            if (learned && (e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;
+            if ((e = hipMemsetAsync(W2.lvl + LVL_UNDER, 0, 2 * sizeof(uint32_t), st2)) != hipSuccess) break;
         }
         // the frame flags (and, for progress, level counts) of both pools, read back after both streams idle
         auto read_flags = [&]() -> hipError_t {
             hipError_t r;
             if (dual && ((r = hipEventRecord(ev_end, st2)) != hipSuccess || (r = hipStreamWaitEvent(st, ev_end, 0)) != hipSuccess))
                 return r;
-            if (learned) {
-                if ((r = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
-                if (dual && (r = hipMemcpyAsync(h_lvl + 64, W2.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
-                    return r;
-            }
+            if ((r = hipMemcpyAsync(h_lvl, W.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
+            if (dual && (r = hipMemcpyAsync(h_lvl + 64, W2.lvl, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return r;
             return hipStreamSynchronize(st);
         };
         auto flagged = [&](int k) { return h_lvl[k] != 0 || (dual && h_lvl[64 + k] != 0); };
@@ -731,8 +743,9 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             if (hybrid) {  // level L: its live chains (<= cap)
                 for (int L = 0; L < A.max_depth; ++L) {
                     b[L] = L == 0 ? np : cap;
-                    if (L > 0 && !conservative && L < (int)wf.frac.size())
-                        b[L] = std::min(cap, (size_t)((double)np * wf.frac[L] * margin) + slack);
+                    if (L > 0 && !conservative && L < (int)wf.frac.size())  // (at least one block: a launch that
+                        // can set LVL_UNDER for every level chains may continue into, even at a learned count of 0)
+                        b[L] = std::min(cap, std::max<size_t>(256, (size_t)((double)np * wf.frac[L] * margin) + slack));
                 }
                 return b;
             }
@@ -740,15 +753,18 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             for (int L = 0; L < A.max_depth && ub > 0; ++L) {
                 b[L] = ub;
                 if (!conservative && L < (int)wf.frac.size())
-                    b[L] = std::min(ub, (size_t)((double)np * wf.frac[L] * margin) + slack);
+                    b[L] = std::min(ub, std::max<size_t>(256, (size_t)((double)np * wf.frac[L] * margin) + slack));
                 ub = L + 1 < A.max_depth ? std::min(ub * (size_t)S.max_children, level_cap) : 0;
             }
             return b;
         };
         const uint64_t total = (uint64_t)npix_total * A.spp;
         uint64_t done = 0;
-        bool stop = false;
-        for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess && !stop; s0 += nsb) {
+        // stop: the callback aborted the frame.  redo_now: a progress check found a batch poisoned -- the frame is
+        // redone at once instead of after its last batch, so that every pass is reported exactly once and from a
+        // clean frame (a multi-rank caller keeps its collectives in step on the passes, tiles.render_progressive)
+        bool stop = false, redo_now = false;
+        for (uint32_t s0 = 0; s0 < (uint32_t)A.spp && e == hipSuccess && !stop && !redo_now; s0 += nsb) {
             const uint32_t nb = std::min<uint32_t>(nsb, (uint32_t)A.spp - s0);
             for (uint32_t p0 = 0; p0 < npix_total; p0 += npix, ++bi) {
                 const bool odd = dual && (bi & 1);
@@ -781,7 +797,11 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     // inside their pixel loop (renderers.js:28-37): here after a batch, when a callback is
                     // due (the host's timelimit clock is checked first: no sync otherwise)
                     if ((e = read_flags()) != hipSuccess) break;
-                    const bool clean = !learned || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
+                    const bool clean = !flagged(LVL_FLAG) && !flagged(LVL_UNDER);
+                    if (!clean) {
+                        redo_now = true;
+                        break;
+                    }
                     const double c = (double)done / (double)total;
                     if (c > reported) {
                         reported = c;
@@ -803,7 +823,11 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             }
             if (e == hipSuccess && progress && A.kind == JSRT_RENDERER_INCREMENTAL && (!due || due())) {  // wait for the pass
                 if ((e = read_flags()) != hipSuccess) break;
-                const bool clean = !learned || (!flagged(LVL_FLAG) && !flagged(LVL_UNDER));
+                const bool clean = !flagged(LVL_FLAG) && !flagged(LVL_UNDER);
+                if (!clean) {
+                    redo_now = true;
+                    break;
+                }
                 const double c = (double)done / (double)total;
                 if (c > reported) {
                     reported = c;
@@ -811,13 +835,23 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                 }
             }
         }
-        if (e == hipSuccess && dual && !learned) {  // st waits for the side stream's batches
-            if ((e = hipEventRecord(ev_end, st2)) == hipSuccess) e = hipStreamWaitEvent(st, ev_end, 0);
+        if (e != hipSuccess) break;
+        if (stop) {  // an aborted frame is not redone (read_flags joins the side stream into st first)
+            e = read_flags();
+            break;
         }
-        if (e != hipSuccess || !learned) break;
+        // The frame flags of both pools, every schedule.  read_flags also joins the side stream into st, so the
+        // caller's stream orders after every batch of the frame (k_final below, and the caller's own work after
+        // jsrt_render_device returns).  A frame that ended with a batch poisoned is redone, never returned: in
+        // the round-4 draft of the hybrid chain this loop broke out for every chain-layout schedule before
+        // reading the flags, so a hybrid frame whose side chains outgrew their slots came back with its
+        // poisoned batches' pixels missing (tests/test_gpu_redo_streams.py).
         if ((e = read_flags()) != hipSuccess) break;
         if (!flagged(LVL_FLAG) && !flagged(LVL_UNDER)) break;
-        if (flagged(LVL_FLAG)) {  // a batch outgrew the pool: twice the pool, relearn the counts
+        if (!learned) {  // chain: only k_shade's k_fix_dirs records can run out (fix_record)
+            if (wf.fix_all) { e = hipErrorOutOfMemory; break; }  // (never: a record per ray slot and level)
+            wf.fix_all = true;
+        } else if (flagged(LVL_FLAG)) {  // a batch outgrew the pool: twice the pool, relearn the counts
             if (paths * wf.pool_factor > ((size_t)1 << 31) * (hybrid ? 4 : 1)) { e = hipErrorOutOfMemory; break; }
             wf.pool_factor *= 2;
             wf.frac.clear();

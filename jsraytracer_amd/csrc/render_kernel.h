@@ -129,6 +129,7 @@ struct Wavefront {  // owns the batch buffers (cached per scene)
     // hybrid: paths + paths x pool_factor / 4 chain slots) and level counts
     size_t pool_paths = 0, pool_factor = 8;
     int pool_mode = -1;
+    bool fix_all = false;  // k_fix_dirs records for every ray slot (a frame ran out of the default 1/8)
     std::vector<double> frac;  // level L ray count / paths of the first batch
     size_t cap_bytes = 0;
     WArgs args{};

@@ -126,20 +126,39 @@ class Scene:
         return rgba, colors, st.as_dict()
 
     def render_device(self, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0, col_block=1, stats=True, progress=None,
-                      **kw):
+                      progress_ex=None, **kw):
         """Render owned columns into device buffers (see jsrt.h jsrt_render_device).  stats=False
         records no per-launch HIP events (and returns None).  progress(pass, completion): called at the
         timelimit_ms cadence with the device buffers holding the running mean of the passes done (Incremental;
-        jsrt_render_device_progress) -- synchronous, the stream idle in the callback."""
+        jsrt_render_device_progress) -- synchronous, the stream idle in the callback.
+        progress_ex(pass, completion, clean) -> truthy to abort (jsrt_render_device_progress_ex): called for every
+        reported pass, clean or not (the multi-rank form, tiles.render_progressive); an exception it raises
+        aborts the frame and is re-raised here."""
         L = _native.lib()
         p = self.params(device=self.device, **kw)
         st = Stats() if stats else None
-        if progress is None:
+        if progress is None and progress_ex is None:
             rc = L.jsrt_render_device(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr, stream_ptr,
                                       ctypes.byref(st) if stats else None)
             check(rc, "jsrt_render_device")
             return st.as_dict() if stats else None
         err = []
+        if progress_ex is not None:
+            def tramp_ex(pass_, completion, clean, _user):
+                try:
+                    return 1 if progress_ex(int(pass_), float(completion), bool(clean)) else 0
+                except BaseException as e:  # noqa: BLE001 -- re-raised after the frame
+                    err.append(e)
+                    return 1
+            cb = _native.PROGRESS_EX_FN(tramp_ex)
+            rc = L.jsrt_render_device_progress_ex(self._h, ctypes.byref(p), col_block, d_rgba_ptr, d_colors_ptr,
+                                                  stream_ptr, cb, None, ctypes.byref(st) if stats else None)
+            if err:
+                raise err[0]
+            if rc == _native.RC_ABORTED:
+                return None
+            check(rc, "jsrt_render_device_progress_ex")
+            return st.as_dict() if stats else None
 
         def tramp(pass_, completion, _user):
             try:

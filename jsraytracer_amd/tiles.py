@@ -77,34 +77,69 @@ def render_progressive(scene, fg, dev_tile, on_preview, timelimit_ms=0.0, host_t
     `timelimit` tick (src/worker.js:30-32, src/renderers.js:103-112) and the main thread overlays them
     (src/raytrace_launcher.js:92-97).  Every rank renders its tile with jsrt_render_device_progress, one
     sample per pixel per pass, so its device tile holds the running mean of passes 0..p at each callback.
-    Rank 0's clock decides whether a preview is due (one broadcast per pass keeps the ranks' collectives in
+    Rank 0's clock decides whether a preview is due (one all-reduce per pass keeps the ranks' collectives in
     step); when it is, the ranks' tiles are gathered (FrameGather, RCCL over xGMI or gloo) and rank 0 gets
     on_preview(pass, image [H, W] int32 RGBA8).  The frame's final tile is left in dev_tile.
 
-    kw: jsrt_render_device parameters (width, height, spp, max_depth, kind, seed, x_offset, x_delt)."""
+    kw: jsrt_render_device parameters (width, height, spp, max_depth, kind, seed, x_offset, x_delt).
+
+    Every rank calls back for the same passes (jsrt_render_device_progress_ex reports each pass, clean or not,
+    and a rank that owns no column reports them too), and each callback runs ONE all-reduce of the ranks'
+    status {a batch poisoned (that tile is not the pass's running mean), a failure, a preview due by rank 0's
+    clock, a rank done}: a preview is gathered only when every tile is clean, and a failure on any rank stops
+    every rank's frame together (the failing rank re-raises, the others raise JsrtError).  A rank leaves with
+    one closing all-reduce (done = 1) unless a progress all-reduce already met a done peer's closing one: every
+    all-reduce of one rank is matched by exactly one of every other rank, so none is left waiting."""
     import time
 
     import torch
     import torch.distributed as dist
     last = [time.perf_counter()]
-    flag = torch.zeros(1, dtype=torch.int32, device="cpu" if host_tiles or fg.world == 1 else dev_tile.device)
+    dev = "cpu" if host_tiles or fg.world == 1 else dev_tile.device
+    status = torch.zeros(4, dtype=torch.int32, device=dev)  # unclean, failed, due, done: max over ranks
+    failed, closed, peer_failed = [], [False], [False]
 
-    def cb(p, _completion):
-        if fg.rank == 0:
-            now = time.perf_counter()
-            due = (now - last[0]) * 1e3 >= timelimit_ms
-            if due:
-                last[0] = now
-            flag.fill_(1 if due else 0)
+    def exchange(unclean, due, done):
+        status.copy_(torch.tensor([unclean, 1 if failed else 0, due, done], dtype=torch.int32))
         if fg.world > 1:
-            dist.broadcast(flag, src=0)
-        if not int(flag.item()):
-            return
-        fg.local.copy_(dev_tile.view(-1)[:fg.local.numel()].to(fg.local.device))
-        img = fg.gather()
+            dist.all_reduce(status, op=dist.ReduceOp.MAX)
+        return [int(x) for x in status.tolist()]
+
+    def cb(p, _completion, clean):
+        due = 0
         if fg.rank == 0:
-            on_preview(p, img)
+            due = 1 if (time.perf_counter() - last[0]) * 1e3 >= timelimit_ms else 0
+        unclean, fail, due_all, done = exchange(0 if clean else 1, due, 0)
+        if done:  # a peer has left its render (it failed): this all-reduce was its closing one
+            closed[0] = True
+            peer_failed[0] = True
+            return True
+        if fail:
+            peer_failed[0] = True
+            return True  # abort this rank's frame (every rank sees the same status)
+        if unclean or not due_all:
+            return False
+        if fg.rank == 0:
+            last[0] = time.perf_counter()
+        try:
+            fg.local.copy_(dev_tile.view(-1)[:fg.local.numel()].to(fg.local.device))
+            img = fg.gather()
+            if fg.rank == 0:
+                on_preview(p, img)
+        except Exception as e:  # noqa: BLE001 -- reported to the peers at the next exchange, re-raised below
+            failed.append(e)
+        return False
 
     # every pass calls back on every rank (a 1e-9 ms library cadence); the preview cadence is rank 0's
-    scene.render_device(dev_tile.data_ptr(), progress=cb, timelimit_ms=1e-9, samples_per_launch=1, stats=False,
-                        col_block=fg.cb, **kw)
+    try:
+        scene.render_device(dev_tile.data_ptr(), progress_ex=cb, timelimit_ms=1e-9, samples_per_launch=1, stats=False,
+                            col_block=fg.cb, **kw)
+    except Exception as e:  # noqa: BLE001 -- this rank's render failed: its peers learn it below
+        failed.append(e)
+    if not closed[0] and exchange(0, 0, 1)[1]:  # the closing exchange: a failure in the last pass reaches all
+        peer_failed[0] = True
+    if failed:
+        raise failed[0]
+    if peer_failed[0]:
+        from ._native import JsrtError
+        raise JsrtError("render_progressive: another rank's render or progress callback failed; frame aborted")

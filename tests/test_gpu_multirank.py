@@ -65,7 +65,7 @@ def test_gpu_rank_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
 PSPP = 4  # progressive frame: passes 0..PSPP-2 call back, the last pass is the final frame
 
 
-def _rank_progressive(rank, world, port, cb, outdir):
+def _rank_progressive(rank, world, port, cb, outdir, W=W, H=H):
     import sys
     sys.path.insert(0, ROOT)
     import torch
@@ -93,20 +93,21 @@ def _rank_progressive(rank, world, port, cb, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cb", [(2, 16), (3, 8)])
-def test_gpu_progressive_previews_gather_to_running_mean(tmp_path, world, cb):
+@pytest.mark.parametrize("world,cb,w", [(2, 16, W), (3, 8, W), (3, 16, 32)])
+def test_gpu_progressive_previews_gather_to_running_mean(tmp_path, world, cb, w):
     """The multi-GPU tile path with progress (jsrt_render_device_progress + tiles.render_progressive): at
     every pass p the ranks' tiles hold the running mean of samples 0..p (renderers.js:93-112), rank 0
     gathers them, and the composite equals the single-rank frame of spp = p + 1 bit for bit (keyed RNG:
-    sample k of a pixel does not depend on spp); the final gather equals the full frame."""
+    sample k of a pixel does not depend on spp); the final gather equals the full frame.  (3, 16, 32): rank 2
+    owns no column (jsrt_render_device_progress_ex still reports its passes, so its collectives keep step)."""
     import jsraytracer_amd as jr
     from oracle import pyoracle
-    mp.start_processes(_rank_progressive, args=(world, _free_port(), cb, str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_rank_progressive, args=(world, _free_port(), cb, str(tmp_path), w, H), nprocs=world, join=True,
                        start_method="spawn")
     sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
     for p in range(PSPP - 1):
         got = np.load(os.path.join(tmp_path, f"pass{p}.npy"))
-        ref, _, _ = sc.render(W, H, p + 1, DEPTH, 1, 1, want_colors=False)
+        ref, _, _ = sc.render(w, H, p + 1, DEPTH, 1, 1, want_colors=False)
         assert np.array_equal(got, ref), f"pass {p}: {int((got != ref).any(-1).sum())} pixels differ"
-    full, _, _ = sc.render(W, H, PSPP, DEPTH, 1, 1, want_colors=False)
+    full, _, _ = sc.render(w, H, PSPP, DEPTH, 1, 1, want_colors=False)
     assert np.array_equal(np.load(os.path.join(tmp_path, "final.npy")), full)

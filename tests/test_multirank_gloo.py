@@ -83,15 +83,16 @@ class _OracleTileScene:
     Incremental renderer's image after pass p) and calls progress after every pass but the last, as
     jsrt_render_device_progress does."""
 
-    def __init__(self, blob, tile, W, H, cols):
+    def __init__(self, blob, tile, W, H, cols, fail_at=None, unclean_at=None):
         self.blob, self.tile, self.W, self.H, self.cols = blob, tile, W, H, cols
+        self.fail_at, self.unclean_at = fail_at, unclean_at  # (test hooks: a failing / poisoned pass)
 
-    def render_device(self, ptr, progress=None, timelimit_ms=0.0, samples_per_launch=0, stats=False, col_block=1,
+    def render_device(self, ptr, progress_ex=None, timelimit_ms=0.0, samples_per_launch=0, stats=False, col_block=1,
                       width=0, height=0, spp=1, max_depth=4, kind=1, seed=1, x_offset=0, x_delt=1):
         import torch
 
         from oracle import pyoracle
-        assert samples_per_launch == 1 and timelimit_ms > 0 and progress is not None
+        assert samples_per_launch == 1 and timelimit_ms > 0 and progress_ex is not None
         for p in range(spp):
             t = np.zeros((len(self.cols), self.H), np.uint32)
             for c, px in enumerate(self.cols):
@@ -100,11 +101,15 @@ class _OracleTileScene:
                 t[c] = rgba[:, px].view(np.uint32).reshape(self.H)
             self.tile.zero_()
             self.tile[:t.size].copy_(torch.from_numpy(t.view(np.int32).reshape(-1)))
-            if p < spp - 1:
-                progress(p, (p + 1) / spp)
+            if p == self.fail_at:
+                raise RuntimeError(f"injected failure at pass {p}")
+            if p < spp - 1 and progress_ex(p, (p + 1) / spp, p != self.unclean_at):
+                return None  # aborted (jsrt_render_device_progress_ex returns -4)
 
 
-def _progressive_worker(rank, world, port, W, H, cb, spp, outdir):
+def _progressive_worker(rank, world, port, W, H, cb, spp, outdir, fail=None, unclean=None, preview_fail=None):
+    """fail / unclean: (rank, pass) whose render raises / whose pass is reported unclean; preview_fail: a pass
+    at which rank 0's on_preview raises.  Each rank writes its outcome to outdir/rank<r>.txt."""
     import sys
     sys.path.insert(0, ROOT)
     import torch
@@ -116,28 +121,63 @@ def _progressive_worker(rank, world, port, W, H, cb, spp, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     fg = FrameGather(W, H, rank, world, cb)
     tile = torch.zeros(fg.maxcols * H, dtype=torch.int32)
-    sc = _OracleTileScene(pyoracle.golden_scene("cornell_box_path"), tile, W, H, owned_px(W, rank, world, cb))
+    sc = _OracleTileScene(pyoracle.golden_scene("cornell_box_path"), tile, W, H, owned_px(W, rank, world, cb),
+                          fail_at=fail[1] if fail and fail[0] == rank else None,
+                          unclean_at=unclean[1] if unclean and unclean[0] == rank else None)
 
     def keep(p, img):
+        if p == preview_fail:
+            raise ValueError(f"injected preview failure at pass {p}")
         np.save(os.path.join(outdir, f"pass{p}.npy"), FrameGather.to_rgba8(img))
 
-    render_progressive(sc, fg, tile, keep, timelimit_ms=0.0, host_tiles=True, width=W, height=H, spp=spp, max_depth=8,
-                       kind=1, seed=5, x_offset=rank, x_delt=world)
+    try:
+        render_progressive(sc, fg, tile, keep, timelimit_ms=0.0, host_tiles=True, width=W, height=H, spp=spp,
+                           max_depth=8, kind=1, seed=5, x_offset=rank, x_delt=world)
+        out = "ok"
+    except Exception as e:  # noqa: BLE001
+        out = type(e).__name__
+    with open(os.path.join(outdir, f"rank{rank}.txt"), "w") as f:
+        f.write(out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cb", [(2, 8), (3, 4)])
-def test_gloo_progressive_previews(tmp_path, world, cb):
-    """tiles.render_progressive on CPU ranks: one broadcast per pass keeps the ranks' gathers in step, and
+def _run_progressive(tmp_path, world, cb, W, spp, **kw):
+    mp.start_processes(_progressive_worker, args=(world, _free_port(), W, W, cb, spp, str(tmp_path), kw.get("fail"),
+                                                  kw.get("unclean"), kw.get("preview_fail")),
+                       nprocs=world, join=True, start_method="spawn")
+    return [open(os.path.join(tmp_path, f"rank{r}.txt")).read() for r in range(world)]
+
+
+@pytest.mark.parametrize("world,cb,W", [(2, 8, 16), (3, 4, 16), (3, 8, 16)])
+def test_gloo_progressive_previews(tmp_path, world, cb, W):
+    """tiles.render_progressive on CPU ranks: one all-reduce per pass keeps the ranks' gathers in step, and
     each pass's gathered preview is the single-process spp = p + 1 frame (oracle tiles; on the GPU the tiles
-    come from jsrt_render_device_progress, tests/test_gpu_multirank.py)."""
+    come from jsrt_render_device_progress_ex, tests/test_gpu_multirank.py).  (3, 8, 16): rank 2 owns no
+    column and still takes part in every pass."""
     from oracle import pyoracle
-    W = H = 16
     spp = 3
-    mp.start_processes(_progressive_worker, args=(world, _free_port(), W, H, cb, spp, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    assert _run_progressive(tmp_path, world, cb, W, spp) == ["ok"] * world
     blob = pyoracle.golden_scene("cornell_box_path")
     for p in range(spp - 1):
-        _, ref, _ = pyoracle.render(blob, W, H, p + 1, 8, 1, 5, 0, 1, threads=1)
+        _, ref, _ = pyoracle.render(blob, W, W, p + 1, 8, 1, 5, 0, 1, threads=1)
         assert np.array_equal(np.load(os.path.join(tmp_path, f"pass{p}.npy")), ref), f"pass {p}"
+
+
+def test_gloo_progressive_unclean_pass_is_not_previewed(tmp_path):
+    """A pass that one rank reports unclean (a poisoned batch: its tile is not the running mean) is previewed
+    by no rank; the other passes are."""
+    assert _run_progressive(tmp_path, 2, 8, 16, 4, unclean=(1, 1)) == ["ok", "ok"]
+    assert [os.path.exists(os.path.join(tmp_path, f"pass{p}.npy")) for p in range(3)] == [True, False, True]
+
+
+@pytest.mark.parametrize("kw,expect", [
+    ({"fail": (1, 0)}, ["JsrtError", "RuntimeError"]),          # rank 1's render fails in pass 0
+    ({"fail": (0, 2)}, ["RuntimeError", "JsrtError"]),          # rank 0's fails after the last reported pass
+    ({"preview_fail": 0}, ["ValueError", "JsrtError"]),         # rank 0's on_preview raises
+    ({"preview_fail": 1}, ["ValueError", "JsrtError"]),         # ... in the last reported pass
+])
+def test_gloo_progressive_failure_reaches_every_rank(tmp_path, kw, expect):
+    """A failure on one rank (its render, or rank 0's preview callback) ends every rank's render_progressive with
+    an exception instead of leaving its peers blocked in a collective (the test would time out)."""
+    assert _run_progressive(tmp_path, 2, 8, 16, 3, **kw) == expect

@@ -11,4 +11,5 @@ timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_$TAG.j
 cat gpurun_out/bench_$TAG.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
     python bench.py --steps 3 --warmup 1 --no-cpu-baseline --events > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err || exit $?
-find gpurun_out/prof_$TAG -name "*kernel_stats*" -exec cat {} \;
+python tools/stamp_stats.py gpurun_out/bench_prof_$TAG.json gpurun_out/prof_$TAG/run_kernel_stats.csv cornell_box_path || exit 1
+cat gpurun_out/prof_$TAG/run_kernel_stats.csv

@@ -11,5 +11,6 @@ for CFG in "$@"; do
   cat gpurun_out/bench_${TAG}_$CFG.json
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$CFG -o run -- \
       python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --events > gpurun_out/bench_prof_${TAG}_$CFG.json 2> gpurun_out/prof_${TAG}_$CFG.err || exit $?
+  python tools/stamp_stats.py gpurun_out/bench_prof_${TAG}_$CFG.json gpurun_out/prof_${TAG}_$CFG/run_kernel_stats.csv $CFG || exit 1
   head -4 gpurun_out/prof_${TAG}_$CFG/run_kernel_stats.csv
 done
