@@ -66,8 +66,10 @@ SIMDS = 256 * 4
 # half the f32 rate 4; transcendentals 4x their type's rate)
 ISSUE_CYC = {"f64": 4.0, "trans_f64": 16.0, "trans_f32": 8.0, "other": 2.0}
 TOL = 1e-5                  # north_star: RGB L-inf on the f32 colour handed to setColor
-# Whether FETCH_SIZE counts 4-B-per-lane coalesced loads at their full bytes on gfx950 (tools/fetch_calib.hip;
-# set from its committed measurement, profiles/fetch_calib_r05.txt)
+# Whether FETCH_SIZE counts 4-B-per-lane coalesced loads at their full bytes on gfx950.  Measured (tools/fetch_calib.hip,
+# profiles/fetch_calib_r05.json, 1 GiB streams): FETCH_SIZE reads 0.500 of the bytes of 4-B and of 16-B coalesced
+# loads alike, WRITE_SIZE 1.000 of coalesced 4-B and 16-B stores, and a lone 4-B store to a line costs 32 B (one
+# 32-B sector) -- so the x2 on FETCH_SIZE holds for this path's SoA planes too.
 FETCH_4B_EXACT = False
 
 
@@ -252,8 +254,8 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame, bu
     if pmc:
         n = pmc["dispatches"]
         # FETCH_SIZE (KB): MI355X_MICROARCH.md reads 1/2 of the bytes of wide (16 B/lane) coalesced streaming
-        # loads on gfx950; other widths are uncalibrated.  This path's loads are mostly 4-B SoA planes, whose
-        # calibration (tools/fetch_calib.hip, profiles/fetch_calib_*.txt) decides which reading is `traffic`.
+        # loads on gfx950; the calibration of this path's 4-B SoA planes (FETCH_4B_EXACT above) decides which
+        # reading is `traffic`; both are reported.
         raw = (pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n
         x2 = (2 * pmc.get("FETCH_SIZE", 0) + pmc.get("WRITE_SIZE", 0)) * 1024 / n
         traffic = raw if FETCH_4B_EXACT else x2
