@@ -181,12 +181,13 @@ JSRT_HD F3 ray_point(F3 o, F3 d, double t) {
 __device__ __forceinline__ void sin_cos(double x, double &s, double &c) { fdlibm::sin_cos(x, s, c); }
 // Vec.spherePick() (math.js:180-185): theta = 2 pi r0, phi = acos(2 r1 - 1), the point (cos theta sin phi,
 // cos phi, sin theta sin phi) as f32, with V8's sin / cos / acos (fdlibm.h).  Only the three f32 roundings
-// reach the image, so OCML's sincos and acos (inlined twice, fdlibm costs k_shade ~70 spilled VGPRs) are
-// evaluated first and kept when every value within SPHERE_PICK_EPS = 2^-44 of each product rounds to the
-// same f32: tests/test_gpu_trig.py bounds |OCML - V8| by 2^-50 on the spherePick arguments of node's fixture,
-// so a product is within 3 * 2^-50 + 2^-52 of V8's, 19x inside the margin, and a kept result is V8's.  The
-// rest (|value| below ~2^-20, or within 2^-44 of an f32 rounding boundary: about one pick in 10^5) are
-// recomputed with fdlibm, out of line.
+// reach the image, so estimates are evaluated first -- OCML's sincos of theta, and sin / cos of phi from
+// sin_cos_of_acos (no acos, no second sincos) -- and kept when every value within SPHERE_PICK_EPS = 2^-44 of
+// each product rounds to the same f32: tests/test_gpu_trig.py bounds |OCML - V8| by 2^-50 on the spherePick
+// arguments of node's fixture and tests/test_sphere_pick_identity.py the phi estimates by 2^-50, so a product
+// is within 3 * 2^-50 + 2^-52 of V8's, 19x inside the margin, and a kept result is V8's.  The rest (|value|
+// below ~2^-20, or within 2^-44 of an f32 rounding boundary: about one pick in 10^5) are recomputed with
+// fdlibm, out of line.
 constexpr double SPHERE_PICK_EPS = 0x1p-44;
 // Whether every value within SPHERE_PICK_EPS of d rounds to d's f32, on the bits of d (|d| <= 2; integer
 // operations, no f64 temporaries; tests/test_box_any.py::test_f32_stable_bits): the f32
@@ -204,6 +205,17 @@ JSRT_HD bool f32_stable_bits(double d) {
 struct SinCos2 {
     double st, ct, sp, cp;
 };
+// sin(phi) and cos(phi) of phi = acos(a) for the filter (not V8's values): sqrt((1 - a)(1 + a)) and a.  Both
+// factors of 1 - a^2 are exact where it matters (Sterbenz: the small one near a = +-1), so the root is within
+// ~2^-52 relative of the real sin(acos(a)), and V8's sin(acos(a)) / cos(acos(a)) are within ~2^-51 of the real
+// values (acos's last-bit error carried through slopes <= 1, plus their own rounding): the approximation is
+// within 2^-50 of V8's, as OCML's acos + sincos were (tests/test_sphere_pick_identity.py checks it against the
+// oracle's fdlibm on 4 M arguments and the poles), so the 2^-44 stability margin still decides exactly.  An
+// acos and a sincos less per pick.
+__device__ __forceinline__ void sin_cos_of_acos(double a, double &sin_phi, double &cos_phi) {
+    sin_phi = sqrt((1.0 - a) * (1.0 + a));
+    cos_phi = a;
+}
 __device__ __forceinline__ SinCos2 sphere_pick_exact(double theta, double a) {
     SinCos2 r;
     fdlibm::sin_cos(theta, r.st, r.ct);
@@ -219,7 +231,7 @@ __device__ __forceinline__ F3 sphere_pick(R &rng) {
     const bool fast = false;
 #else
     sincos(theta, &sin_t, &cos_t);
-    sincos(::acos(a), &sin_phi, &cos_phi);
+    sin_cos_of_acos(a, sin_phi, cos_phi);
     const bool fast = f32_stable_bits(cos_t * sin_phi) && f32_stable_bits(cos_phi) && f32_stable_bits(sin_t * sin_phi);
 #endif
     if (__builtin_expect(!fast, 0)) {  // out of line: the hot path keeps OCML's register footprint
@@ -238,7 +250,7 @@ __device__ __forceinline__ F3 sphere_pick_fast(R &rng, bool &unstable) {
     const double a = 2.0 * rng.next() - 1.0;
     double sin_t, cos_t, sin_phi, cos_phi;
     sincos(theta, &sin_t, &cos_t);
-    sincos(::acos(a), &sin_phi, &cos_phi);
+    sin_cos_of_acos(a, sin_phi, cos_phi);
     const double px = cos_t * sin_phi, pz = sin_t * sin_phi;
     unstable = !(f32_stable_bits(px) && f32_stable_bits(cos_phi) && f32_stable_bits(pz));  // (forced: JSRT_FORCE_EXACT_PICK)
     return f3((float)px, or0((float)cos_phi), or0((float)pz));

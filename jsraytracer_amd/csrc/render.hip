@@ -557,13 +557,16 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
     const char *pe = getenv("JSRT_PERSIST");
     const bool persist = (S.profile & PF_SDF) && S.all_roots_prims && !(pe && pe[0] == '0');
-    // A frame that fits one batch of 32 M paths or more (a rank's columns of a two-GPU render) is cut into
-    // two batches of half the samples, so that they run on the two batch streams (below): cornell at
-    // 1024^2 x 32 +3.6 %; at 16 M paths the halves lose 5 % (profiles/r03_s18_ab.txt s28), so smaller frames
-    // stay whole.  JSRT_SPLIT_FRAME=0 keeps one batch.
-    const char *sf = getenv("JSRT_SPLIT_FRAME");
+    // A frame that fits one batch of 4 M paths or more (a rank's columns of a multi-GPU render) is cut into
+    // two batches of half the samples, so that they run on the two batch streams (below).  Round 3 split only
+    // from 32 M paths (cornell 1024^2 x 32 +3.6 %; halves of 16 M lost 5 %, profiles/r03_s18_ab.txt s28); with
+    // the hybrid chain the halves win down to 4 M: cornell's 4-rank share (16.7 M paths) 32.0 -> 29.5 ms, its
+    // 8-rank share (8.4 M) 17.0 -> 16.3 ms (tools/project_scaling.py, profiles/r05_s6_projection.txt).
+    // JSRT_SPLIT_FRAME=0 keeps one batch; JSRT_SPLIT_MIN=k (A/B) splits from 2^k paths.
+    const char *sf = getenv("JSRT_SPLIT_FRAME"), *sm = getenv("JSRT_SPLIT_MIN");  // (A/B: log2 of the paths)
+    const int split_min = sm ? std::max(1, std::min(40, atoi(sm))) : 22;
     if (!persist && !(sf && sf[0] == '0') && npix == npix_total && nsb == (uint32_t)A.spp && A.spp >= 2 &&
-        (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << 25))
+        (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << split_min))
         nsb = (uint32_t)((A.spp + 1) / 2);  // odd spp: halves of (spp + 1) / 2 and (spp - 1) / 2 samples
     // Chain schedule when no node can have two children: depth x paths node records, nothing can
     // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all

@@ -910,19 +910,30 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     }
     if (nchild > 0 && unit_child(ch0)) out.info |= INFO_UNIT0;
     if (nchild > 1 && unit_child(ch1)) out.info |= INFO_UNIT1;
+    // (JSRT_X_*: timing-only experiments that drop one class of k_shade's stores; the image is wrong)
+#ifndef JSRT_X_NONODE
     store_node(W, i, out.surf, out.info & ~INFO_FIX);
+#endif
+#ifndef JSRT_X_NOHAND
+    // (The record at the node's own index -- coalesced 16-B stores -- with k_shadow gathering it through hnode:
+    // k_shade -1.5 ms, k_shadow +2.9 ms per cornell frame, profiles/r05_s5_s6_ab.txt; the scatter stays here.)
     if (out.info & INFO_LIT) {
         if (!W.bucket) store_hand(W, q, out.h);
         else if (hslot != ~0u) store_hand(W, hslot, out.h);
     }
+#endif
+#ifndef JSRT_X_NONODE
     if (nchild > 0) store_child(W, i, 0, ch0);
     if (nchild > 1) store_child(W, i, 1, ch1);
+#endif
     if (CHAIN) {  // the child ray (World.color(child, depth - 1)) takes over slot q
         uint32_t *next = (L & 1) ? W.list0 : W.list1;  // level L + 1's list
         if (child_depth > 0 && nchild > 0) {
+#ifndef JSRT_X_NORAY
             W.ox[r] = out.h.pos.x; W.oy[r] = out.h.pos.y; W.oz[r] = out.h.pos.z;
             W.dx[r] = ch0.dir.x; W.dy[r] = ch0.dir.y; W.dz[r] = ch0.dir.z;
             W.addr[r] = mix32(out.h.addr, 1u);
+#endif
             if (W.hybrid) next[at] = r;
         } else {
             W.prim[r] = NO_RAY;  // no child, or children black without a cast (depth 0)
