@@ -166,7 +166,15 @@ struct DScene {
     const uint64_t *grid_mask;   // grid_cells + 1 entries
     float grid_lo[3], grid_inv[3];
     int32_t grid_dim[3], grid_cells, grid_masked, pad_grid;
+    // The shading tables k_shade reads per hit (prims, prim_shade, shade0, shadeI, mat, mat_flags, mc, mc_const,
+    // prim_lit) packed into one image of stab_words 16-B words (0: too big for LDS), at byte offsets stab_off[k]
+    // in that order: k_shade copies it into LDS, so a hit's dependent record chain (prim -> matrix / material ->
+    // colour constants) is LDS round trips instead of L2 ones (render_levels.h k_shade).
+    const void *stab;            // 16-B aligned
+    int32_t stab_words;
+    int32_t stab_off[9];
 };
+constexpr int STAB_MAX_WORDS = 1024;  // 16 KB of LDS at most
 
 // Dynamic LDS of a casting kernel over a scene with BVHs: per lane a traversal stack of bvh_stack
 // 4-byte entries (device_common.h bvh_cast).

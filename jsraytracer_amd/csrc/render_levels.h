@@ -53,6 +53,30 @@
 
 namespace jsrt {
 
+#ifdef JSRT_X_STAMPS
+// (timing experiment only) per-phase shader-clock cycles of k_shade: every 16th block's waves add each phase's
+// cycles into their own slot (no atomics: same-address atomics from many waves would serialise and swamp the
+// kernel), g_xst[slot][k] and the count in [slot][8 + k]; jsrt_x_stamps (render_pf.hip) sums the slots
+constexpr int XST_SLOTS = 32768;
+static __device__ unsigned long long g_xst[XST_SLOTS][16];
+template <class T>
+__device__ __forceinline__ void xst(int k, uint64_t &t, const T &dep) {
+    asm volatile("" ::"v"(dep));  // the phase ends when `dep` is available
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    const uint32_t slot = (blockIdx.x >> 4) * 4 + (threadIdx.x >> 6);
+    if (__lane_id() == 0 && (blockIdx.x & 15) == 0 && slot < XST_SLOTS) {
+        g_xst[slot][k] += (unsigned long long)(now - t);
+        g_xst[slot][8 + k] += 1ull;
+    }
+    t = now;
+}
+#define XST_BEGIN uint64_t xst_t = __builtin_amdgcn_s_memtime();
+#define XST(k, dep) xst(k, xst_t, dep)
+#else
+#define XST_BEGIN
+#define XST(k, dep)
+#endif
+
 constexpr uint32_t NO_PARENT = 0xFFFFFFFFu;  // camera ray: its result is the path's root colour
 constexpr uint32_t DEAD_RAY = 0xFFFFFFFEu;   // level-0 slot of a path outside the image (no result)
 constexpr int32_t NO_RAY = -2;                // W.prim of a slot that holds no ray to trace
@@ -776,14 +800,17 @@ __device__ __forceinline__ void fix_record(const WArgs &W, const uint32_t *fixl,
 // a 416-B stack frame per lane; either slowed k_shade 25 % to 4x, profiles/r04_s10_ab.txt, r04_s11_ab.txt).
 __global__ __launch_bounds__(256) void k_fix_dirs(WArgs W);
 
-template <int PF, bool CHAIN>
+// STAGE (flat scenes whose shading tables fit, DScene::stab): the tables are copied into LDS by every block, so a
+// hit's dependent record chain (prim -> shading matrix / material -> colour constants) is LDS round trips
+template <int PF, bool CHAIN, bool STAGE>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
     DScene S, WArgs W, int L, int child_depth) {
+    XST_BEGIN
     const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
     const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
     const uint32_t count = R.count, base = R.base, next_base = CHAIN ? 0u : R.base + R.count;
-    if (!CHAIN || W.hybrid) {
-        if (t0 >= count) return;  // block-uniform: every thread of a live block reaches block_append
+    if (!CHAIN || W.hybrid || STAGE) {
+        if (t0 >= count) return;  // block-uniform: every thread of a live block reaches block_append / the barrier
     } else if (tt >= count) {
         return;
     }
@@ -833,6 +860,38 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
     __shared__ uint32_t fixl[5 * 256];  // shade_node's unstable spherePicks (INFO_FIX)
     const int prim = in ? W.prim[r] : NO_RAY;
     const bool hit = prim >= 0;
+    // STAGE: the ray (and its hit) loaded before the staging barrier, so the two latencies overlap (without it
+    // the loads stay under `hit`: hoisted there they cost the mesh / SDF k_shade ~40 spilled VGPRs)
+    F3 ro = f3(0, 0, 0), rd = f3(0, 0, 0);
+    double rt = 0;
+    int32_t rctx = 0;
+    uint32_t raddr = 0, rkey = 0;
+    if (STAGE && in) {
+        ro = f3(W.ox[r], W.oy[r], W.oz[r]);
+        rd = f3(W.dx[r], W.dy[r], W.dz[r]);
+        rt = W.t[r];
+        rctx = W.ctx[r];
+        raddr = W.addr[r];
+        rkey = W.key[r];
+    }
+    DScene SL = S;
+    if constexpr (STAGE) {
+        extern __shared__ uint4 stab_lds[];
+        const uint4 *src = reinterpret_cast<const uint4 *>(S.stab);
+        for (int k = (int)threadIdx.x; k < S.stab_words; k += 256) stab_lds[k] = src[k];
+        __syncthreads();
+        const char *sb = reinterpret_cast<const char *>(stab_lds);
+        SL.prims = reinterpret_cast<const DPrim *>(sb + S.stab_off[0]);
+        SL.prim_shade = reinterpret_cast<const int32_t *>(sb + S.stab_off[1]);
+        SL.shade0 = reinterpret_cast<const double *>(sb + S.stab_off[2]);
+        SL.shadeI = reinterpret_cast<const double *>(sb + S.stab_off[3]);
+        SL.mat = reinterpret_cast<const jsrt_rec_material *>(sb + S.stab_off[4]);
+        SL.mat_flags = reinterpret_cast<const int32_t *>(sb + S.stab_off[5]);
+        SL.mc = reinterpret_cast<const jsrt_rec_mcolor *>(sb + S.stab_off[6]);
+        SL.mc_const = reinterpret_cast<const float *>(sb + S.stab_off[7]);
+        SL.prim_lit = reinterpret_cast<const int32_t *>(sb + S.stab_off[8]);
+    }
+    XST(0, prim);
     // Every load, and the children's append (a returning atomic), is issued before the node's first
     // store: vmcnt counts stores too, in issue order, so a load or atomic issued behind the node's
     // ~20 HBM stores would wait for all of them to complete.
@@ -842,9 +901,16 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         path = W.path[r];
     }
     if (hit) {
-        const F3 o = f3(W.ox[r], W.oy[r], W.oz[r]), d = f3(W.dx[r], W.dy[r], W.dz[r]);
-        const Hit h{W.t[r], prim, W.ctx[r]};
-        nchild = shade_node<PF>(S, W.ns > 0, h, o, d, W.addr[r], W.key[r], out, ch0, ch1, fixl, W.force_fix != 0);
+        if (!STAGE) {
+            ro = f3(W.ox[r], W.oy[r], W.oz[r]);
+            rd = f3(W.dx[r], W.dy[r], W.dz[r]);
+            rt = W.t[r];
+            rctx = W.ctx[r];
+            raddr = W.addr[r];
+            rkey = W.key[r];
+        }
+        const Hit h{rt, prim, rctx};
+        nchild = shade_node<PF>(SL, W.ns > 0, h, ro, rd, raddr, rkey, out, ch0, ch1, fixl, W.force_fix != 0);
         out.h.node = CHAIN ? slot : q;  // (k_shadow: node base + this)
         out.h.mask = (uint32_t)S.grid_cells;  // every root
         if (W.bucket && (out.info & INFO_LIT)) {  // the lit node's hand-off slot, ranked by k_extend
@@ -856,6 +922,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
             if (W.bucket_grid) out.h.mask = (uint32_t)b;
         }
     }
+    XST(1, out.info);
     // tree: children append to level L + 1; at depth 0 they are black without a cast
     // W.child_sort: a block's children grouped by direction octant, so a wave of the next level's k_extend
     // casts rays of one or two octants that walk the same BVH subtrees (WArgs::child_sort)
@@ -877,6 +944,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         block_append2(W.lvl + 2 * (L + 1), cont, side, at, side_at);
         side_at += side_base(W, L + 1);
     }
+    XST(2, side_at);
     // unstable spherePicks: the record for k_fix_dirs, with the slots the children's rays go to below (written
     // before the node's stores, behind which the returning atomic would wait for all of them)
     if (__builtin_expect(hit && (out.info & INFO_FIX) != 0u, 0) && child_depth > 0) {
@@ -952,6 +1020,10 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
             W.parent[c] = i;
             W.prim[c] = -1;
         }
+#ifdef JSRT_X_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);  // (the stores retired)
+        XST(3, r);
+#endif
         return;
     }
     if (nchild == 0) return;
@@ -1310,7 +1382,11 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
         if (W.bucket) hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(256), 0, st, W, L);
         if (split && L > 0 && W.ns > 0) (void)hipStreamWaitEvent(st, sync->shadow_done, 0);  // the hand-off is free
         timed(KT_SHADE, [&] {
-            hipLaunchKernelGGL((k_shade<PF, CHAIN>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
+            if (PF == PF_ANALYTIC && S.stab_words > 0)  // the LDS-staged shading tables
+                hipLaunchKernelGGL((k_shade<PF, CHAIN, PF == PF_ANALYTIC>), dim3(grid_ub(ub)), dim3(256), (size_t)S.stab_words * 16,
+                                   st, S, W, L, child_depth);
+            else
+                hipLaunchKernelGGL((k_shade<PF, CHAIN, false>), dim3(grid_ub(ub)), dim3(256), 0, st, S, W, L, child_depth);
             if (child_depth > 0) hipLaunchKernelGGL(k_fix_dirs, dim3(1), dim3(256), 0, st, W);
         });
         if (W.ns > 0 && split) {

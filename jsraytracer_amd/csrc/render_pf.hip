@@ -28,3 +28,16 @@ template void material_data_pf<JSRT_PF>(const DScene &, const float *, uint32_t,
                                         float *, float *, float *, hipStream_t);
 #endif
 }  // namespace jsrt
+
+#if defined(JSRT_X_STAMPS) && JSRT_PF == 0 && JSRT_PART == 0
+// (timing experiment only) the per-phase cycle sums of the analytic chain k_shade (render_levels.h g_xst),
+// and reset them
+extern "C" int jsrt_x_stamps(unsigned long long *out) {
+    std::vector<unsigned long long> h((size_t)jsrt::XST_SLOTS * 16);
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(jsrt::g_xst), h.size() * 8) != hipSuccess) return -1;
+    for (int k = 0; k < 16; ++k) out[k] = 0;
+    for (size_t i = 0; i < h.size(); ++i) out[i % 16] += h[i];
+    std::fill(h.begin(), h.end(), 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(jsrt::g_xst), h.data(), h.size() * 8) == hipSuccess ? 0 : -1;
+}
+#endif
