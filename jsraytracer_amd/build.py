@@ -84,12 +84,36 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _src_stamp(deps, cmd):
+    """Content hash of an object's sources and its compile command (the object's .src sidecar): an object is
+    rebuilt when its inputs' contents differ, whatever the mtimes say (a tool that rewrites an object in place,
+    or a copy that keeps old mtimes, must not let a stale object into the library)."""
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _obj_stale(o, deps, cmd):
+    if not os.path.exists(o) or not os.path.exists(o + ".src"):
+        return True
+    with open(o + ".src") as f:
+        return f.read().strip() != _src_stamp(deps, cmd)
+
+
 def _obj(stem, tag=""):
     return os.path.join(OUT, f"{stem}{tag}.o")
 
 
 def _deps(src, deps):
     return [os.path.join(CSRC, src)] + [_path(d) for d in deps]
+
+
+def _cmd(src, defs, extra, o):
+    """The hipcc command line of one object (the .tmp output is renamed over `o` once it succeeds)."""
+    dev = [] if "-DJSRT_MACHINE_LICM" in extra or not src.endswith(".hip") else NO_MLICM
+    return [HIPCC] + OBJ_FLAGS + dev + defs + list(extra) + ["-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
 
 
 def _stale():
@@ -101,7 +125,8 @@ def _stale():
             return True  # built from other sources (mtimes do not survive every copy; the id does)
     if not any(os.path.exists(o) for o in objs):
         return False  # a prebuilt library shipped without its objects (the GPU box's snapshot), same id: use it
-    return any(_newer(_obj(stem), _deps(src, deps)) for stem, src, _, deps in UNITS) or _newer(LIB, objs)
+    return any(_obj_stale(_obj(stem), _deps(src, deps), _cmd(src, defs, [], _obj(stem)))
+               for stem, src, defs, deps in UNITS) or _newer(LIB, objs)
 
 
 def build(force=False, verbose=False, variant=None, defines=(), profiles=None):
@@ -128,23 +153,25 @@ def _build_locked(force, verbose, variant, defines, profiles):
         mine = variant is not None and (profiles is None or any(stem.startswith(f"render_pf{p}_") for p in profiles))
         o = _obj(stem, tag if mine else "")
         objs.append(o)
-        if force or mine or _newer(o, _deps(src, deps)):
-            extra = list(defines) if mine else []
-            dev = [] if "-DJSRT_MACHINE_LICM" in extra or not src.endswith(".hip") else NO_MLICM
-            cmd = [HIPCC] + OBJ_FLAGS + dev + defs + extra + ["-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
-            jobs.append((cmd, o))
+        extra = list(defines) if mine else []
+        cmd = _cmd(src, defs, extra, o)
+        if force or mine or _obj_stale(o, _deps(src, deps), cmd):
+            jobs.append((cmd, o, _src_stamp(_deps(src, deps), cmd)))
 
     def run(job):
-        cmd, o = job
+        cmd, o, stamp = job
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         os.replace(o + ".tmp", o)
+        if stamp is not None:
+            with open(o + ".src", "w") as f:
+                f.write(stamp + "\n")
 
     bid = build_id(defines if variant is not None else ())
     id_src = _write_id_unit(bid, tag)
     id_obj = _obj("build_id", tag)
-    jobs.append(([HIPCC] + OBJ_FLAGS + ["-c", id_src, "-o", id_obj + ".tmp"], id_obj))
+    jobs.append(([HIPCC] + OBJ_FLAGS + ["-c", id_src, "-o", id_obj + ".tmp"], id_obj, None))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with ThreadPoolExecutor(workers) as ex:
         list(ex.map(run, jobs))

@@ -166,13 +166,17 @@ struct DScene {
     const uint64_t *grid_mask;   // grid_cells + 1 entries
     float grid_lo[3], grid_inv[3];
     int32_t grid_dim[3], grid_cells, grid_masked, pad_grid;
-    // The shading tables k_shade reads per hit (prims, prim_shade, shade0, shadeI, mat, mat_flags, mc, mc_const,
-    // prim_lit) packed into one image of stab_words 16-B words (0: too big for LDS), at byte offsets stab_off[k]
-    // in that order: k_shade copies it into LDS, so a hit's dependent record chain (prim -> matrix / material ->
-    // colour constants) is LDS round trips instead of L2 ones (render_levels.h k_shade).
+    // The per-hit tables of k_shade and k_shadow packed into one image of stab_words 16-B words (0: too big for
+    // LDS), table k at byte offset stab_off[k] (STAB_*).  k_shade copies all of it into LDS and k_shadow the
+    // prefix of its own tables (stab_words_shadow words), so a hit's dependent record chain (prim -> matrix /
+    // material -> colour constants) is LDS round trips instead of L2 ones (render_levels.h k_shade, k_shadow).
     const void *stab;            // 16-B aligned
-    int32_t stab_words;
-    int32_t stab_off[9];
+    int32_t stab_words, stab_words_shadow;
+    int32_t stab_off[12];
+};
+enum {  // DScene::stab tables, in image order: k_shadow's first (mat .. sample_light), then k_shade's
+    STAB_MAT, STAB_MAT_FLAGS, STAB_MC, STAB_MC_CONST, STAB_SAMPLE_CALL, STAB_SAMPLE_LIGHT,
+    STAB_PRIMS, STAB_PRIM_SHADE, STAB_SHADE0, STAB_SHADEI, STAB_PRIM_LIT, STAB_N
 };
 constexpr int STAB_MAX_WORDS = 1024;  // 16 KB of LDS at most
 

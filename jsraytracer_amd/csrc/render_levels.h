@@ -800,6 +800,24 @@ __device__ __forceinline__ void fix_record(const WArgs &W, const uint32_t *fixl,
 // a 416-B stack frame per lane; either slowed k_shade 25 % to 4x, profiles/r04_s10_ab.txt, r04_s11_ab.txt).
 __global__ __launch_bounds__(256) void k_fix_dirs(WArgs W);
 
+// DScene::stab: the per-hit tables in LDS (`lds`, a copy of the image or of k_shadow's prefix of it) bound in the
+// kernel's own DScene copy in place of the global ones
+__device__ __forceinline__ void stab_bind(DScene &SL, const uint4 *lds, bool shade) {
+    const char *sb = reinterpret_cast<const char *>(lds);
+    SL.mat = reinterpret_cast<const jsrt_rec_material *>(sb + SL.stab_off[STAB_MAT]);
+    SL.mat_flags = reinterpret_cast<const int32_t *>(sb + SL.stab_off[STAB_MAT_FLAGS]);
+    SL.mc = reinterpret_cast<const jsrt_rec_mcolor *>(sb + SL.stab_off[STAB_MC]);
+    SL.mc_const = reinterpret_cast<const float *>(sb + SL.stab_off[STAB_MC_CONST]);
+    SL.sample_call = reinterpret_cast<const int32_t *>(sb + SL.stab_off[STAB_SAMPLE_CALL]);
+    SL.sample_light = reinterpret_cast<const int32_t *>(sb + SL.stab_off[STAB_SAMPLE_LIGHT]);
+    if (!shade) return;
+    SL.prims = reinterpret_cast<const DPrim *>(sb + SL.stab_off[STAB_PRIMS]);
+    SL.prim_shade = reinterpret_cast<const int32_t *>(sb + SL.stab_off[STAB_PRIM_SHADE]);
+    SL.shade0 = reinterpret_cast<const double *>(sb + SL.stab_off[STAB_SHADE0]);
+    SL.shadeI = reinterpret_cast<const double *>(sb + SL.stab_off[STAB_SHADEI]);
+    SL.prim_lit = reinterpret_cast<const int32_t *>(sb + SL.stab_off[STAB_PRIM_LIT]);
+}
+
 // STAGE (flat scenes whose shading tables fit, DScene::stab): the tables are copied into LDS by every block, so a
 // hit's dependent record chain (prim -> shading matrix / material -> colour constants) is LDS round trips
 template <int PF, bool CHAIN, bool STAGE>
@@ -880,16 +898,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT
         const uint4 *src = reinterpret_cast<const uint4 *>(S.stab);
         for (int k = (int)threadIdx.x; k < S.stab_words; k += 256) stab_lds[k] = src[k];
         __syncthreads();
-        const char *sb = reinterpret_cast<const char *>(stab_lds);
-        SL.prims = reinterpret_cast<const DPrim *>(sb + S.stab_off[0]);
-        SL.prim_shade = reinterpret_cast<const int32_t *>(sb + S.stab_off[1]);
-        SL.shade0 = reinterpret_cast<const double *>(sb + S.stab_off[2]);
-        SL.shadeI = reinterpret_cast<const double *>(sb + S.stab_off[3]);
-        SL.mat = reinterpret_cast<const jsrt_rec_material *>(sb + S.stab_off[4]);
-        SL.mat_flags = reinterpret_cast<const int32_t *>(sb + S.stab_off[5]);
-        SL.mc = reinterpret_cast<const jsrt_rec_mcolor *>(sb + S.stab_off[6]);
-        SL.mc_const = reinterpret_cast<const float *>(sb + S.stab_off[7]);
-        SL.prim_lit = reinterpret_cast<const int32_t *>(sb + S.stab_off[8]);
+        stab_bind(SL, stab_lds, true);
     }
     XST(0, prim);
     // Every load, and the children's append (a returning atomic), is issued before the node's first
@@ -1064,8 +1073,8 @@ __device__ __forceinline__ F3 mc_const3(const DScene &S, int m) {  // a constant
     return f3(c.x, c.y, c.z);
 }
 template <int PF, bool SPH = true>
-__device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
-    const float4 h0 = hp[0], h1 = hp[hs];
+__device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 &h0, const float4 &h1, const float4 *hp,
+                                                size_t hs, uint32_t s, F3 &P, F3 &delta) {
     P = f3(h0.x, h0.y, h0.z);
     RngH rng{f2u(h0.w), (uint32_t)S.sample_call[s]};
     F3 L, lcol;
@@ -1098,10 +1107,15 @@ __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *h
 __device__ __forceinline__ bool shadowed(const Hit &sh) { return sh.prim >= 0 && sh.t > 0 && sh.t < 1; }
 
 template <int PF, bool SPH = true>
-__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 *hp, size_t hs, uint32_t s,
-                                           uint64_t mask = ~0ull) {
+__device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *hp, size_t hs, uint32_t s, F3 &P, F3 &delta) {
+    return sample_unshadowed<PF, SPH>(S, hp[0], hp[hs], hp, hs, s, P, delta);
+}
+
+template <int PF, bool SPH = true>
+__device__ __forceinline__ F3 sample_color(const DScene &S, const float4 &h0, const float4 &h1, const float4 *hp,
+                                           size_t hs, uint32_t s, uint64_t mask = ~0ull) {
     F3 P, delta;
-    const F3 c = sample_unshadowed<PF, SPH>(S, hp, hs, s, P, delta);
+    const F3 c = sample_unshadowed<PF, SPH>(S, h0, h1, hp, hs, s, P, delta);
     // A shadowed sample contributes +0.  An unshadowed one whose colour is +-0 in every component
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
@@ -1130,7 +1144,10 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
     return ret;
 }
 
-template <int PF, bool CHAIN, bool SERIAL, bool SPH>
+// STAGE (flat scenes, DScene::stab; not SERIAL): k_shadow's tables (materials, colour constants, light-sample
+// indices) copied into LDS by every block behind its hand-off loads, so a sample's material -> colour chain is
+// LDS round trips
+template <int PF, bool CHAIN, bool SERIAL, bool SPH, bool STAGE = false>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(
     DScene S, WArgs W, int L) {
     const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
@@ -1171,14 +1188,26 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSR
             const DLight &Lt = S.lights[li];
             const int n = Lt.kind == JSRT_LIGHT_POINT ? 1 : Lt.samples;
             F3 light_color = f3(0, 0, 0);
-            for (int j = 0; j < n; ++j, ++k) light_color = add(light_color, sample_color<PF, SPH>(S, hp, W.hstride, k, mask));
+            for (int j = 0; j < n; ++j, ++k)
+                light_color = add(light_color, sample_color<PF, SPH>(S, hp[0], hp[W.hstride], hp, W.hstride, k, mask));
             if (n > 0) ret = add(ret, scale(light_color, Lt.inv_n));  // times(1 / samples)
         }
         W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
         return;
     }
     F3 c = f3(0, 0, 0);
-    if (lit && s < ns) c = sample_color<PF, SPH>(S, hp, W.hstride, s, mask);
+    const float4 h0 = hp[0], h1 = hp[W.hstride];  // (loaded by every lane: before the staging barrier)
+    if constexpr (STAGE) {
+        extern __shared__ uint4 stab_lds[];
+        const uint4 *src = reinterpret_cast<const uint4 *>(S.stab);
+        for (int k = (int)threadIdx.x; k < S.stab_words_shadow; k += 256) stab_lds[k] = src[k];
+        __syncthreads();
+        DScene SL = S;
+        stab_bind(SL, stab_lds, false);
+        if (lit && s < ns) c = sample_color<PF, SPH>(SL, h0, h1, hp, W.hstride, s, mask);
+    } else {
+        if (lit && s < ns) c = sample_color<PF, SPH>(S, h0, h1, hp, W.hstride, s, mask);
+    }
     ret = light_sums(S, G, ret, c);
     if (lit && s == 0) W.node[i] = make_float4(ret.x, ret.y, ret.z, nd.w);
 }
@@ -1407,10 +1436,16 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                                            dim3(persistent_grid((const void *)k_shadow_cast<PF, CHAIN, false>, ne)), dim3(256), 0, st, S, W, L);
                     hipLaunchKernelGGL((k_shadow_sum<CHAIN>), dim3(grid_ub(ne)), dim3(256), 0, st, S, W, L);
                 } else if (W.ns <= 1 || W.group > 1) {
-                    if (S.sphere_lights)
-                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
+                    const dim3 g(grid_ub(ub * (size_t)W.group));
+                    const size_t sl = (size_t)S.stab_words_shadow * 16;  // the LDS-staged tables (flat scenes)
+                    if (PF == PF_ANALYTIC && sl && S.sphere_lights)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);
+                    else if (PF == PF_ANALYTIC && sl)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);
+                    else if (S.sphere_lights)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true>), g, dim3(256), lds, st, S, W, L);
                     else
-                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false>), dim3(grid_ub(ub * (size_t)W.group)), dim3(256), lds, st, S, W, L);
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false>), g, dim3(256), lds, st, S, W, L);
                 } else if (S.sphere_lights) {
                     hipLaunchKernelGGL((k_shadow<PF, CHAIN, true, true>), dim3(grid_ub(ub)), dim3(256), lds, st, S, W, L);
                 } else {

@@ -7,6 +7,7 @@ instructions a kernel's code holds (static, not executed counts).
 """
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -17,7 +18,10 @@ B = "/opt/rocm/lib/llvm/bin"
 def disasm(obj):
     with tempfile.TemporaryDirectory() as t:
         fat, co = os.path.join(t, "fat.bin"), os.path.join(t, "k.co")
-        subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+        # (on a copy: llvm-objcopy with no output file rewrites its input, which would touch the object's mtime)
+        src = os.path.join(t, "obj.o")
+        shutil.copyfile(obj, src)
+        subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", src], check=True)
         subprocess.run([f"{B}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
         return subprocess.run([f"{B}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True, capture_output=True,

@@ -4,6 +4,7 @@
 """
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -16,7 +17,10 @@ KEYS = ("name", "vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "s
 def notes(obj):
     with tempfile.TemporaryDirectory() as t:
         fat, co = os.path.join(t, "fat.bin"), os.path.join(t, "k.co")
-        subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+        # (on a copy: llvm-objcopy with no output file rewrites its input, which would touch the object's mtime)
+        src = os.path.join(t, "obj.o")
+        shutil.copyfile(obj, src)
+        subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", src], check=True)
         subprocess.run([f"{B}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
         return subprocess.run([f"{B}/llvm-readobj", "--notes", co], check=True, capture_output=True, text=True).stdout
