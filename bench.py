@@ -319,6 +319,10 @@ def main():
                          "events and one instrumented one-stream step follows them")
     ap.add_argument("--spp", type=int, default=0, help="profiling only: override the config's spp (same launch "
                     "shapes, fewer batches); a bench line with it is not the config's number")
+    ap.add_argument("--gather", choices=["rgba8", "accum"], default="rgba8",
+                    help="the multi-GPU exchange: packed RGBA8 tiles (4 B per pixel, the reference workers' ImageData), "
+                         "or the f32 accumulators (16 B per pixel) finished by one k_final on rank 0 "
+                         "(jsrt_render_device_accum, tiles.AccumGather); the image is the same bit for bit")
     ap.add_argument("--ab", action="store_true", help="allow JSRT_* environment knobs / JSRT_LIB variants (A/B runs; "
                     "the line records them under `knobs`)")
     args = ap.parse_args()
@@ -348,7 +352,7 @@ def main():
             dist.init_process_group(backend)
 
     import jsraytracer_amd as jr
-    from jsraytracer_amd.tiles import FrameGather
+    from jsraytracer_amd.tiles import AccumGather, FrameGather
     from oracle import pyoracle  # fixture loader only; the oracle runs only in the cpu_baseline / parity legs
 
     scene_name, W, H, spp, kind, depth, bound = CONFIGS[args.config]
@@ -371,12 +375,24 @@ def main():
     STAGES = jr._native.STAGES
     ONE = jr._native.EVENTS_ONE_STREAM  # instrumented steps: every stage's own launch times (one stream)
 
+    accum = args.gather == "accum"
+    if accum:  # the accumulator exchange: f32 tiles gathered to rank 0, finished there by one k_final
+        ag = AccumGather(W, H, rank, world, cb, device="cpu" if host_tiles else f"cuda:{local}")
+        atile = torch.zeros_like(ag.local, device=f"cuda:{local}") if host_tiles else ag.local
+
     def step(events=None, colors=None):
         """events: None = no HIP events; 0 = every stage; else a bitmask of stages (jsrt.h stage_events)."""
-        st = scene.render_device(tile.data_ptr(), colors.data_ptr() if colors is not None else None,
-                                 stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp, max_depth=depth,
-                                 kind=kind, seed=1, x_offset=rank if world > 1 else 0, x_delt=world,
-                                 stats=events is not None, stage_events=events or 0)
+        kw = dict(stream_ptr=stream, col_block=cb, width=W, height=H, spp=spp, max_depth=depth, kind=kind, seed=1,
+                  x_offset=rank if world > 1 else 0, x_delt=world, stats=events is not None, stage_events=events or 0)
+        if accum:
+            st = scene.render_device_accum(atile.data_ptr(), **kw)
+            if host_tiles:
+                ag.local.copy_(atile.cpu())
+            acc = ag.gather()
+            if rank == 0:
+                fg.image.copy_(AccumGather.finish(acc.to(f"cuda:{local}"), kind, spp).to(fg.image.device))
+            return st
+        st = scene.render_device(tile.data_ptr(), colors.data_ptr() if colors is not None else None, **kw)
         if host_tiles:
             fg.local.copy_(tile.cpu())
         fg.gather()
@@ -391,7 +407,8 @@ def main():
     # duration for the roofline); events on every launch would add launch gaps to the step.  The last
     # timed step also writes the f32 colours handed to setColor (k_final, 16 B per pixel): the parity
     # block checks that frame itself.
-    colors = torch.empty(fg.maxcols * H * 4, dtype=torch.float32, device=f"cuda:{local}") if world == 1 else None
+    colors = torch.empty(fg.maxcols * H * 4, dtype=torch.float32, device=f"cuda:{local}") \
+        if world == 1 and not accum else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -452,7 +469,7 @@ def main():
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth} (Incremental)", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"tiles{world}",
                        "col_block": cb, "headline": args.config == HEADLINE and args.spp == 0,
-                       "gather_backend": backend if world > 1 else None},
+                       "gather_backend": backend if world > 1 else None, "gather": args.gather},
             "roofline": roof, "cpu_baseline": cpu, "parity": par,
             "build_id": jr._native.build_id(), "knobs": knobs(),
             "kernel_ms_per_step": kernel_ms,

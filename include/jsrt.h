@@ -102,19 +102,36 @@ int jsrt_render_device(jsrt_scene *scene, const jsrt_params *params, int32_t col
 int jsrt_render_device_progress(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
                                 float *d_colors, void *hip_stream, jsrt_progress_fn progress, void *user,
                                 jsrt_stats *stats);
-/* (jsrt_render / jsrt_render_device_progress call back on clean passes only: a pass of a batch that outgrew
- * its device pool or launch bound -- the frame is then redone after its last batch, and passes already
- * reported are not reported again -- is skipped, so a callback never sees a stale preview.) */
+/* (Every callback sees a clean preview: the progress check that finds a batch outgrew its device pool or
+ * launch bound redoes the frame at once, before that pass is reported, and passes already reported are not
+ * reported again -- each pass is reported once, from a clean frame.) */
 
 /* The multi-rank form of jsrt_render_device_progress (jsraytracer_amd/tiles.py render_progressive): progress
- * is called for EVERY pass the frame reports, clean = 1 when the device tile holds that pass's running mean
- * (0: a batch was poisoned; the tile is not a preview), so every rank calls back the same passes and can keep
- * its collectives in step (a rank that owns no column still reports each pass).  A non-zero return aborts the
- * frame: the call returns -4 ("render aborted by the progress callback") once the device is idle. */
+ * is called for every pass the frame reports with clean = 1 when the device tile holds that pass's running
+ * mean (always, as above; the flag is kept so a caller never has to assume it), so every rank calls back the
+ * same passes and can keep its collectives in step (a rank that owns no column still reports each pass).  A
+ * non-zero return aborts the frame: the call returns -4 ("render aborted by the progress callback") once the
+ * device is idle. */
 typedef int32_t (*jsrt_progress_ex_fn)(int32_t pass, double completion, int32_t clean, void *user);
 int jsrt_render_device_progress_ex(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, uint32_t *d_rgba8,
                                    float *d_colors, void *hip_stream, jsrt_progress_ex_fn progress, void *user,
                                    jsrt_stats *stats);
+
+/* jsrt_render_device with the renderer's f32 accumulator as the output (the multi-GPU accumulator exchange,
+ * jsraytracer_amd/tiles.py AccumGather): d_accum (ncols * H * 4 f32, laid out as d_rgba8 with 4 floats per pixel,
+ * w = 0) receives each owned pixel's accumulator before setColor -- Incremental: the f32 sum of its samples in
+ * order (renderers.js:93-97), RandomMultisampling: the sum of sample / spp (renderers.js:52-62), Simple: the
+ * sample.  No RGBA8 is written.  Asynchronous w.r.t. the host. */
+int jsrt_render_device_accum(jsrt_scene *scene, const jsrt_params *params, int32_t col_block, float *d_accum,
+                             void *hip_stream, jsrt_stats *stats);
+
+/* setColor of n accumulators (device f32 x 4 each, any pixel order, as jsrt_render_device_accum writes them):
+ * the renderer's final colour (kind 1, Incremental: times(1 / passes), renderers.js:98; kinds 0 / 2: the
+ * accumulator) and PixelBuffer.setColor's RGBA8 (pixelbuffer.js:39-49) into d_rgba8 (n u32) and d_colors
+ * (n x 4 f32, nullable) -- the same k_final every render ends with, so a gathered composite's RGBA8 is the
+ * single-GPU frame's bit for bit.  Asynchronous w.r.t. the host. */
+int jsrt_finish_accum(const float *d_accum, int64_t n, int32_t kind, int32_t passes, uint32_t *d_rgba8,
+                      float *d_colors, void *hip_stream);
 
 /* World.cast(ray, min_dist, max_dist, intersect_transparent) (world.js:28-30) of n rays on the scene's
  * device: rays = n x 6 f32 host array (origin xyz with w = 1, direction xyz with w = 0, as

@@ -5,9 +5,9 @@ This package is the Python host side mirroring the reference's renderer interfac
 (src/renderers.js, src/pixelbuffer.js); the Node host side lives in jsraytracer_amd/js/.
 """
 from ._native import JsrtError, LIB_PATH  # noqa: F401
-from .renderer import HipRenderer, PixelBuffer, Scene, owned_columns, scene_header  # noqa: F401
+from .renderer import HipRenderer, PixelBuffer, Scene, finish_accum, owned_columns, scene_header  # noqa: F401
 from .mesh import attach_obj, load_obj_scene  # noqa: F401
 from .serial import blob_from_json, load_json_scene  # noqa: F401
 
-__all__ = ["HipRenderer", "PixelBuffer", "Scene", "JsrtError", "owned_columns", "scene_header", "LIB_PATH",
+__all__ = ["HipRenderer", "PixelBuffer", "Scene", "JsrtError", "finish_accum", "owned_columns", "scene_header", "LIB_PATH",
            "attach_obj", "load_obj_scene", "blob_from_json", "load_json_scene"]

@@ -51,7 +51,8 @@ RC_ABORTED = -4  # jsrt_render_device_progress_ex: the callback asked to stop th
 # exported symbols of include/jsrt.h (checked by tests/test_capi_symbols.py)
 EXPORTS = ["jsrt_scene_create", "jsrt_scene_destroy", "jsrt_render", "jsrt_render_device", "jsrt_cast",
            "jsrt_material_data", "jsrt_sdf_distance", "jsrt_owned_columns", "jsrt_last_error", "jsrt_abi_version",
-           "jsrt_device_count", "jsrt_build_id", "jsrt_render_device_progress", "jsrt_render_device_progress_ex"]
+           "jsrt_device_count", "jsrt_build_id", "jsrt_render_device_progress", "jsrt_render_device_progress_ex",
+           "jsrt_render_device_accum", "jsrt_finish_accum"]
 # exported symbols of include/jsrt_mesh.h (native OBJ ingest + BVH build; host-only, no GPU needed)
 MESH_EXPORTS = ["jsrt_blob_attach_obj", "jsrt_blob_attach_obj_mtl", "jsrt_blob_free"]
 # exported symbols of include/jsrt_json.h (Serializer-JSON reader; host-only)
@@ -122,6 +123,12 @@ def lib():
     L.jsrt_render_device_progress_ex.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, PROGRESS_EX_FN,
                                                  ctypes.c_void_p, ctypes.POINTER(Stats)]
+    L.jsrt_render_device_accum.restype = ctypes.c_int
+    L.jsrt_render_device_accum.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.POINTER(Stats)]
+    L.jsrt_finish_accum.restype = ctypes.c_int
+    L.jsrt_finish_accum.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]
     L.jsrt_cast.restype = ctypes.c_int
     L.jsrt_cast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double, ctypes.c_double,
                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]

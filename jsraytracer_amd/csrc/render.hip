@@ -871,10 +871,25 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     if (h_lvl) (void)hipHostFree(h_lvl);
     release_events();
     if (e != hipSuccess) return e;
+    if (!A.rgba) return hipSuccess;  // the caller takes the accumulator itself (jsrt_render_device_accum)
     const bool ev = kt && kt->on(KT_FINAL);
     if (ev) kt->ev[KT_FINAL].begin(st);
     hipLaunchKernelGGL(k_final, dim3(grid((size_t)A.ncols * A.H)), dim3(256), 0, st, A, (int32_t)A.spp);
     if (ev) kt->ev[KT_FINAL].end(st);
+    return hipGetLastError();
+}
+
+hipError_t finish_accum(const float *accum, size_t n, int kind, int passes, uint32_t *rgba, float *colors, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (!accum || !rgba || passes < 1 || n > (size_t)INT32_MAX) return hipErrorInvalidValue;
+    RenderArgs A{};
+    A.kind = kind;
+    A.ncols = (int32_t)n;
+    A.H = 1;
+    A.accum = const_cast<float *>(accum);
+    A.rgba = rgba;
+    A.colors = colors;
+    hipLaunchKernelGGL(k_final, dim3(grid(n)), dim3(256), 0, st, A, (int32_t)passes);
     return hipGetLastError();
 }
 

@@ -185,6 +185,9 @@ size_t wavefront_bytes_per_path(const DScene &S, int ns, int max_depth);
 // Running mean of the first `passes` samples -> A.rgba / A.colors (k_final with times(1/passes),
 // renderers.js:93-98): the image IncrementalMultisamplingRenderer holds after pass passes-1.
 hipError_t render_preview(const RenderArgs &A, int passes, hipStream_t st);
+// k_final over n accumulators (f32 x 4 each, any pixel order): renderer `kind`'s final colour (Incremental:
+// times(1 / passes)) and PixelBuffer.setColor's RGBA8 (jsrt_finish_accum).
+hipError_t finish_accum(const float *accum, size_t n, int kind, int passes, uint32_t *rgba, float *colors, hipStream_t st);
 
 // World.cast (world.js:28-30) of n rays (device buffers: n x 6 f32 rays, origin w = 1, direction
 // w = 0): closest-hit distance and DPrim index (-1: none).  The jsrt_cast entry (known-answer tests).

@@ -173,11 +173,27 @@ class Scene:
         check(rc, "jsrt_render_device_progress")
         return st.as_dict() if stats else None
 
+    def render_device_accum(self, d_accum_ptr, stream_ptr=0, col_block=1, stats=True, **kw):
+        """Render owned columns into a device f32 accumulator (jsrt.h jsrt_render_device_accum: ncols * H * 4 f32,
+        [owned column][row], w = 0), the multi-GPU accumulator exchange's tile; no RGBA8."""
+        L = _native.lib()
+        p = self.params(device=self.device, **kw)
+        st = Stats() if stats else None
+        check(L.jsrt_render_device_accum(self._h, ctypes.byref(p), col_block, d_accum_ptr, stream_ptr,
+                                         ctypes.byref(st) if stats else None), "jsrt_render_device_accum")
+        return st.as_dict() if stats else None
+
     def header(self):
         return scene_header(self._blob)
 
 
 PROGRESS_NONE = ctypes.cast(None, _native.PROGRESS_FN)
+
+
+def finish_accum(d_accum_ptr, n, kind, passes, d_rgba_ptr, d_colors_ptr=None, stream_ptr=0):
+    """setColor of n device accumulators (jsrt.h jsrt_finish_accum): RGBA8 (+ f32 colours) on a device stream."""
+    check(_native.lib().jsrt_finish_accum(d_accum_ptr, int(n), int(kind), int(passes), d_rgba_ptr, d_colors_ptr,
+                                          stream_ptr), "jsrt_finish_accum")
 
 
 def owned_columns(width, x_offset, x_delt, col_block=1):

@@ -72,6 +72,54 @@ class FrameGather:
         return image.cpu().numpy().view(np.uint8).reshape(image.shape[0], image.shape[1], 4)
 
 
+class AccumGather:
+    """The accumulator exchange: gathers per-rank f32 accumulator tiles ([max_owned * H] pixels x 4 f32, as
+    jsrt_render_device_accum writes them) to rank 0 and permutes them into image order ([H * W] pixels x 4), so
+    rank 0 holds the frame's accumulators -- the f32 state the reference's workers sum their samples into
+    (src/renderers.js:93-97) -- and finishes them with one k_final (jsrt_finish_accum: setColor's RGBA8).
+    Pixels never split across ranks, so the composite accumulators, and the RGBA8 finished from them, are the
+    single-GPU frame's bit for bit.  Four times the RGBA8 exchange's bytes (16 B per pixel), for a caller that
+    combines or re-normalises passes on rank 0.  One collective per frame, like FrameGather."""
+
+    def __init__(self, width, height, rank, world, col_block=1, device="cpu"):
+        import torch
+        self.W, self.H, self.rank, self.world, self.cb = width, height, rank, world, col_block
+        self.ncols = len(owned_px(width, rank, world, col_block))
+        self.maxcols = max_owned(width, world, col_block)
+        self.local = torch.zeros(self.maxcols * height * 4, dtype=torch.float32, device=device)
+        self.parts = [torch.empty_like(self.local) for _ in range(world)] if rank == 0 else None
+        self.slot = torch.as_tensor(column_permutation(width, world, col_block), device=device) if rank == 0 else None
+        self.image = torch.empty((height, width, 4), dtype=torch.float32, device=device) if rank == 0 else None
+
+    def gather(self):
+        """Collective: every rank calls it after its accumulator tile is in self.local.  Returns the [H, W, 4] f32
+        accumulators on rank 0 (image order), None elsewhere."""
+        import torch
+        import torch.distributed as dist
+        if self.world > 1:
+            dist.gather(self.local, self.parts if self.rank == 0 else None, dst=0)
+        else:
+            self.parts = [self.local]
+        if self.rank != 0:
+            return None
+        allc = torch.stack(self.parts).view(self.world * self.maxcols, self.H, 4)  # [slot][row][4]
+        self.image.copy_(allc.index_select(0, self.slot).permute(1, 0, 2))
+        return self.image
+
+    @staticmethod
+    def finish(image, kind, passes):
+        """rank 0: the RGBA8 frame [H, W] int32 (packed) of gathered accumulators [H, W, 4] on a GPU
+        (jsrt_finish_accum, on torch's current stream of that device)."""
+        import torch
+
+        from .renderer import finish_accum
+        acc = image.contiguous()
+        out = torch.empty(acc.shape[0] * acc.shape[1], dtype=torch.int32, device=acc.device)
+        finish_accum(acc.data_ptr(), out.numel(), kind, passes, out.data_ptr(), None,
+                     torch.cuda.current_stream(acc.device).cuda_stream)
+        return out.view(acc.shape[0], acc.shape[1])
+
+
 def render_progressive(scene, fg, dev_tile, on_preview, timelimit_ms=0.0, host_tiles=False, **kw):
     """Progressive multi-rank render of one frame: the reference's workers post their partial image at every
     `timelimit` tick (src/worker.js:30-32, src/renderers.js:103-112) and the main thread overlays them

@@ -1239,6 +1239,7 @@ typedef struct {
     uint32_t seed;
     float *colors;
     uint8_t *rgba;
+    float *accum; /* (nullable) per pixel, W x H x 4: the renderer's f32 accumulator before setColor */
     int tid, nthreads;
     int err;
     char errmsg[512];
@@ -1258,10 +1259,11 @@ static void *render_thread(void *arg) {
         for (int py = 0; py < J->H && !C->err; ++py) {
             const double y = -2 * ((double)py / J->H) + 1;
             C->pixel = (uint32_t)(py * J->W + px);
-            Vec out;
+            Vec out, accv;
             if (J->kind == JSRT_RENDERER_SIMPLE) {
                 C->sample = 0;
                 out = sample_color(C, J->kind, x, y, pw, ph, J->depth);
+                accv = out;
             } else if (J->kind == JSRT_RENDERER_INCREMENTAL) { /* renderers.js:87-98 */
                 Vec buf = vof3(0, 0, 0);
                 for (int it = 0; it < J->spp; ++it) {
@@ -1271,6 +1273,7 @@ static void *render_thread(void *arg) {
                     out = vtimes(buf, 1.0 / (it + 1));
                 }
                 if (J->spp <= 0) continue;
+                accv = buf;
             } else { /* RandomMultisampling getPixelColor (renderers.js:52-62) */
                 Vec acc = vof3(0, 0, 0);
                 for (int s = 0; s < J->spp; ++s) {
@@ -1278,8 +1281,11 @@ static void *render_thread(void *arg) {
                     acc = vplus(acc, vtimes(sample_color(C, J->kind, x, y, pw, ph, J->depth), 1.0 / J->spp));
                 }
                 out = acc;
+                accv = acc;
             }
             set_color(J->rgba, J->colors, J->W, px, py, out);
+            if (J->accum) /* the accumulator's rgb (the kernels' layout carries no w) */
+                for (int k = 0; k < 4; ++k) J->accum[((size_t)py * J->W + px) * 4 + k] = k < 3 && accv.n > k ? accv.v[k] : 0.0f;
         }
     }
     J->err = C->err;
@@ -1291,6 +1297,11 @@ static void *render_thread(void *arg) {
 
 int jsrt_oracle_render(const void *blob, size_t blob_bytes, const jsrt_oracle_params *p, float *colors_out,
                        uint8_t *rgba_out, jsrt_oracle_stats *stats) {
+    return jsrt_oracle_render_accum(blob, blob_bytes, p, colors_out, rgba_out, NULL, stats);
+}
+
+int jsrt_oracle_render_accum(const void *blob, size_t blob_bytes, const jsrt_oracle_params *p, float *colors_out,
+                             uint8_t *rgba_out, float *accum_out, jsrt_oracle_stats *stats) {
     Scene S;
     if (parse_scene(blob, blob_bytes, &S)) return -1;
     const int W = p && p->width > 0 ? p->width : (int)S.rndr->width;
@@ -1316,6 +1327,7 @@ int jsrt_oracle_render(const void *blob, size_t blob_bytes, const jsrt_oracle_pa
         J->seed = p ? p->seed : 1u;
         J->colors = colors_out;
         J->rgba = rgba_out;
+        J->accum = accum_out;
         J->tid = t;
         J->nthreads = nt;
         if (nt == 1) render_thread(J);

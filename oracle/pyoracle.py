@@ -50,6 +50,10 @@ def lib():
         L.jsrt_oracle_render.restype = ctypes.c_int
         L.jsrt_oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(OracleParams),
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(OracleStats)]
+        L.jsrt_oracle_render_accum.restype = ctypes.c_int
+        L.jsrt_oracle_render_accum.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(OracleParams),
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.POINTER(OracleStats)]
         L.jsrt_oracle_last_error.restype = ctypes.c_char_p
         L.jsrt_oracle_fmod.restype = ctypes.c_double
         L.jsrt_oracle_fmod.argtypes = [ctypes.c_double, ctypes.c_double]
@@ -73,8 +77,10 @@ def lib():
     return _lib
 
 
-def render(blob, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, threads=None):
-    """Render with the oracle. Returns (colors f32[H,W,4], rgba u8[H,W,4], stats dict)."""
+def render(blob, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, threads=None,
+           accum=False):
+    """Render with the oracle. Returns (colors f32[H,W,4], rgba u8[H,W,4], stats dict) and, with accum=True, the
+    renderer's f32 accumulators f32[H,W,4] (rgb, w = 0) as a fourth item."""
     L = lib()
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
@@ -86,10 +92,13 @@ def render(blob, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offse
     rgba = np.zeros((H, W, 4), np.uint8)
     st = OracleStats()
     buf = ctypes.create_string_buffer(bytes(blob), len(blob))
-    rc = L.jsrt_oracle_render(buf, len(blob), ctypes.byref(p), colors.ctypes.data, rgba.ctypes.data, ctypes.byref(st))
+    acc = np.zeros((H, W, 4), np.float32) if accum else None
+    rc = L.jsrt_oracle_render_accum(buf, len(blob), ctypes.byref(p), colors.ctypes.data, rgba.ctypes.data,
+                                    acc.ctypes.data if accum else None, ctypes.byref(st))
     if rc != 0:
         raise RuntimeError("oracle: " + L.jsrt_oracle_last_error().decode())
-    return colors, rgba, {n: getattr(st, n) for n in STAT_FIELDS}
+    stats = {n: getattr(st, n) for n in STAT_FIELDS}
+    return (colors, rgba, stats, acc) if accum else (colors, rgba, stats)
 
 
 def scene_header(blob):

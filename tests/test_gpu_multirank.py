@@ -111,3 +111,51 @@ def test_gpu_progressive_previews_gather_to_running_mean(tmp_path, world, cb, w)
         assert np.array_equal(got, ref), f"pass {p}: {int((got != ref).any(-1).sum())} pixels differ"
     full, _, _ = sc.render(w, H, PSPP, DEPTH, 1, 1, want_colors=False)
     assert np.array_equal(np.load(os.path.join(tmp_path, "final.npy")), full)
+
+
+def _rank_accum(rank, world, port, cb, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import jsraytracer_amd as jr
+    from jsraytracer_amd.tiles import AccumGather
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    ag = AccumGather(W, H, rank, world, cb)  # host tiles: gloo gathers CPU tensors
+    dev = torch.zeros(ag.maxcols * H * 4, dtype=torch.float32, device="cuda:0")
+    sc.render_device_accum(dev.data_ptr(), col_block=cb, width=W, height=H, spp=SPP, max_depth=DEPTH, kind=1, seed=1,
+                           x_offset=rank, x_delt=world, stats=False)
+    torch.cuda.synchronize()
+    ag.local.copy_(dev.cpu())
+    acc = ag.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "accum.npy"), acc.numpy())
+        img = AccumGather.finish(acc.to("cuda:0"), 1, SPP)  # one k_final on rank 0
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, "composite.npy"), img.cpu().numpy().view(np.uint8).reshape(H, W, 4))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 16), (3, 8)])
+def test_gpu_accum_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
+    """The accumulator exchange with real HIP tiles (jsrt_render_device_accum per rank, tiles.AccumGather, one
+    jsrt_finish_accum on rank 0): the finished composite equals the 1-rank frame's RGBA8 bit for bit, and its
+    accumulators equal the oracle's on an oracle-sized crop of the frame (src/renderers.js:93-98: the
+    accumulator, then times(1 / passes) and setColor)."""
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    mp.start_processes(_rank_accum, args=(world, _free_port(), cb, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    full, _, _ = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0).render(W, H, SPP, DEPTH, 1, 1,
+                                                                                     want_colors=False)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "composite.npy")), full)
+    acc = np.load(os.path.join(tmp_path, "accum.npy"))
+    _, _, _, ref = pyoracle.render(pyoracle.golden_scene("cornell_box_path"), W, H, SPP, DEPTH, 1, 1, 37, 64,
+                                   accum=True)
+    cols = list(range(37, W, 64))
+    assert np.array_equal(acc[:, cols].view(np.uint32), ref[:, cols].view(np.uint32))

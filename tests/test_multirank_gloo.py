@@ -181,3 +181,43 @@ def test_gloo_progressive_failure_reaches_every_rank(tmp_path, kw, expect):
     """A failure on one rank (its render, or rank 0's preview callback) ends every rank's render_progressive with
     an exception instead of leaving its peers blocked in a collective (the test would time out)."""
     assert _run_progressive(tmp_path, 2, 8, 16, 3, **kw) == expect
+
+
+def _accum_worker(rank, world, port, W, H, cb, spp, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from jsraytracer_amd.tiles import AccumGather, owned_px
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    blob = pyoracle.golden_scene("cornell_box_path")
+    ag = AccumGather(W, H, rank, world, cb)
+    tile = np.zeros((ag.maxcols, H, 4), np.float32)  # [owned column][row][4], as jsrt_render_device_accum
+    for c, px in enumerate(owned_px(W, rank, world, cb)):
+        _, _, _, acc = pyoracle.render(blob, W, H, spp, 8, 1, 5, int(px), W, threads=1, accum=True)
+        tile[c] = acc[:, px]
+    ag.local.copy_(torch.from_numpy(tile.reshape(-1)))
+    img = ag.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "accum.npy"), img.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cb", [(2, 8), (3, 4)])
+def test_gloo_accum_gather_is_the_single_process_accumulator(tmp_path, world, cb):
+    """tiles.AccumGather (the f32 accumulator exchange, jsrt_render_device_accum's tiles): each rank's tile is the
+    oracle's accumulators of its owned columns; the gathered composite must equal the single-process frame's
+    accumulators bit for bit (pixels never split across ranks: each pixel's samples are summed in order on one
+    rank, src/renderers.js:93-97)."""
+    from oracle import pyoracle
+    W = H = 16
+    spp = 3
+    mp.start_processes(_accum_worker, args=(world, _free_port(), W, H, cb, spp, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(os.path.join(tmp_path, "accum.npy"))
+    _, _, _, ref = pyoracle.render(pyoracle.golden_scene("cornell_box_path"), W, H, spp, 8, 1, 5, threads=1, accum=True)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
