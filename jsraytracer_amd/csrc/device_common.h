@@ -418,6 +418,73 @@ JSRT_HD double aabb_intersect(const T *c, const T *h, F3 o, F3 d, double minD, d
     return -(double)__builtin_inf();
 }
 
+// Closest-hit form of the AABB test (World.cast's closest hit, world.js:7-15: a distance is kept only when
+// minD < t < lim, lim = min(maxD, the closest hit so far)), decided in f32 as box_any_f32 with maxD := lim:
+// 0 = not accepted (t_out untouched; the exact test's distance would be rejected), 1 = accepted with the EXACT
+// distance in t_out, -1 = too close to call (the caller runs aabb_intersect).  An accepted distance is one slab
+// quotient -- tmin, the largest lower quotient, when it is above minD, else tmax, the smallest upper one -- so
+// when the f32 estimates single out that axis by more than their error bounds, the exact distance is that
+// axis's correctly rounded f64 quotient (p -+ h) / d: one division instead of aabb_slab's six.  The lower
+// quotient of an axis is (p - h) / d for d > 0 and (p + h) / d for d < 0 (division rounds monotonically, and
+// h >= 0), as aabb_slab's swap leaves it; p = c - o in f32 and p +- h exact in f64, as aabb_slab forms them.
+template <class T>  // T: float in any address space
+JSRT_HD int box_closest_f32(const T *c, const T *h, F3 o, F3 d, const BoxRay &r, double minD, double lim, double &t_out) {
+    constexpr float EPS = 4.76837158203125e-7f, TINY = 1e-30f;  // 2^-21
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    float lo[3], hi[3];
+    float tmin = -__builtin_inff(), tmax = __builtin_inff();
+    int kmin = -1, kmax = -1;
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float p = c[i] - oo[i];
+        lo[i] = -__builtin_inff();
+        hi[i] = __builtin_inff();
+        if ((r.skip >> i) & 1u) {
+            out = out || fabsf(p) > h[i];  // exact: both f32
+        } else {
+            const float a = (p + h[i]) * r.inv[i], b = (p - h[i]) * r.inv[i];
+            lo[i] = fminf(a, b);
+            hi[i] = fmaxf(a, b);
+            if (kmin < 0 || lo[i] > tmin) { tmin = lo[i]; kmin = i; }
+            if (kmax < 0 || hi[i] < tmax) { tmax = hi[i]; kmax = i; }
+        }
+    }
+    if (out) return 0;
+    if (!__builtin_isfinite(tmin) || !__builtin_isfinite(tmax)) return -1;  // (also every axis skipped)
+    const float f0 = (float)minD, f1 = (float)lim;
+    if (!__builtin_isfinite(f0)) return -1;
+    const bool inf1 = !__builtin_isfinite(f1) && f1 > 0;
+    const float en = EPS * fabsf(tmin) + TINY, ex = EPS * fabsf(tmax) + TINY;
+    const float e0 = EPS * fabsf(f0) + TINY, e1 = inf1 ? 0.0f : EPS * fabsf(f1) + TINY;
+    int k = -1;
+    bool lower = true;
+    if (tmin - en > f0 + e0) {  // tmin > minD: t = tmin
+        const bool lt1 = inf1 || tmin + en < f1 - e1, gt1 = !inf1 && tmin - en > f1 + e1;
+        if (gt1 || tmin - en > tmax + ex) return 0;
+        if (!(lt1 && tmin + en < tmax - ex)) return -1;
+        k = kmin;
+    } else if (tmin + en < f0 - e0) {  // tmin < minD: t = tmax
+        const bool lt1 = inf1 || tmax + ex < f1 - e1, gt1 = !inf1 && tmax - ex > f1 + e1;
+        if (tmax + ex < f0 - e0 || gt1) return 0;
+        if (!(tmax - ex > f0 + e0 && lt1)) return -1;
+        k = kmax;
+        lower = false;
+    } else {
+        return -1;
+    }
+    // the extreme quotient's axis, separated from the others by the error bounds
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (j == k || ((r.skip >> j) & 1u)) continue;
+        if (lower ? !(lo[j] + (EPS * fabsf(lo[j]) + TINY) < tmin - en) : !(hi[j] - (EPS * fabsf(hi[j]) + TINY) > tmax + ex))
+            return -1;
+    }
+    const double p = (double)(c[k] - oo[k]), hh = (double)h[k], di = (double)dd[k];
+    t_out = ((di > 0) == lower) ? (p - hh) / di : (p + hh) / di;
+    return 1;
+}
+
 JSRT_HD double plane_t(F3 o, F3 d) {  // geometry.js:246-248
     return (d.z != 0.0f) ? -(double)o.z / (double)d.z : -DINF;
 }
@@ -979,6 +1046,23 @@ JSRT_HD double planar_intersect(int k, const T *inv, F3 o, F3 d, double minD, do
     return (dot3(p, p) <= 1) ? t : -(double)__builtin_inf();  // Circle, geometry.js:310-314
 }
 
+#ifdef JSRT_X_F32XF
+// (timing experiment only) the any-hit filters' local rays from an f32 transform
+template <class T>
+__device__ __forceinline__ float xf_row_point_x(const T *r, F3 o) {
+    return fmaf(o.x, (float)r[0], fmaf(o.y, (float)r[1], fmaf(o.z, (float)r[2], (float)r[3])));
+}
+template <class T>
+__device__ __forceinline__ float xf_row_dir_x(const T *r, F3 d) {
+    return fmaf(d.x, (float)r[0], fmaf(d.y, (float)r[1], d.z * (float)r[2]));
+}
+#define XROWP xf_row_point_x
+#define XROWD xf_row_dir_x
+#else
+#define XROWP xf_row_point
+#define XROWD xf_row_dir
+#endif
+
 // Any-hit acceptance of a SimplePlane / Square / Circle in a shadow cast (planar_intersect's result accepted
 // by minD < t < maxD; `best` is +inf on every lane still casting), decided in f32: 1 = accepted (t_out = the
 // f32 estimate of the distance, inside the bounds by the margin), 0 = not accepted, -1 = too close to call
@@ -989,7 +1073,7 @@ JSRT_HD double planar_intersect(int k, const T *inv, F3 o, F3 d, double minD, do
 template <class T>
 JSRT_HD int planar_any_f32(int k, const T *inv, F3 o, F3 d, double minD, double maxD, double &t_out) {
     constexpr float EPS = 4.76837158203125e-7f, EPSP = 3.814697265625e-6f, TINY = 1e-30f;  // 2^-21, 2^-18
-    const float oz = xf_row_point(inv + 8, o), dz = xf_row_dir(inv + 8, d);
+    const float oz = XROWP(inv + 8, o), dz = XROWD(inv + 8, d);
     if (dz == 0.0f) return 0;  // t = -inf (planar_intersect's dz == 0 case): never accepted
 #ifdef __HIP_DEVICE_COMPILE__
     const float ta = -oz * __builtin_amdgcn_rcpf(dz);  // v_rcp_f32: within 1 ulp
@@ -1006,8 +1090,8 @@ JSRT_HD int planar_any_f32(int k, const T *inv, F3 o, F3 d, double minD, double 
         t_out = ta;
         return 1;
     }
-    const float ox = xf_row_point(inv, o), oy = xf_row_point(inv + 4, o);
-    const float dx = xf_row_dir(inv, d), dy = xf_row_dir(inv + 4, d);
+    const float ox = XROWP(inv, o), oy = XROWP(inv + 4, o);
+    const float dx = XROWD(inv, d), dy = XROWD(inv + 4, d);
     const double td = (double)ta;
     const float sx = (float)((double)dx * td), sy = (float)((double)dy * td);
     const float px = ox + sx, py = oy + sy;
@@ -1044,7 +1128,7 @@ JSRT_HD int planar_any_f32(int k, const T *inv, F3 o, F3 d, double minD, double 
 // 2^-19 (sqrt(disc) / a + |t|) of the exact quotient: the f32 roundings of b, a and the discriminant
 // (2^-24 each), sqrt and rcp (1 ulp each) and the f32 sum (2^-24 (|b| + sqrt(disc))), whose cancellation
 // term is covered by sqrt(disc) / a when it is large and by |t| ~ |b| / a when sqrt(disc) is small.
-JSRT_HD int sphere_any_f32(F3 o, F3 d, double minD, double maxD, double &t_out) {
+JSRT_HD int sphere_any_f32(F3 o, F3 d, double minD, double maxD, double &t_out, bool *second = nullptr) {
     constexpr float EPS = 4.76837158203125e-7f, EPSS = 1.9073486328125e-6f, TINY = 1e-30f;  // 2^-21, 2^-19
     const double a = dot3(d, d), b = dot3(d, o), c = dot3(o, o) - 1;
     const double big = b * b - a * c;
@@ -1067,9 +1151,11 @@ JSRT_HD int sphere_any_f32(F3 o, F3 d, double minD, double maxD, double &t_out) 
     if (t2 - e2 > f0 + em) {  // t2 > minD: t = t2
         t = t2;
         et = e2;
+        if (second) *second = true;
     } else if (t2 + e2 < f0 - em) {  // t2 < minD: t = t1
         t = t1;
         et = e1;
+        if (second) *second = false;
     } else {
         return -1;
     }
@@ -1079,6 +1165,23 @@ JSRT_HD int sphere_any_f32(F3 o, F3 d, double minD, double maxD, double &t_out) 
         return 1;
     }
     return -1;
+}
+
+// Closest-hit form of the Sphere test (sphere_static's distance kept when minD < t < lim), decided by
+// sphere_any_f32 with maxD := lim: 0 = not accepted, 1 = accepted with the EXACT distance in t_out -- the root
+// sphere_any_f32 settled on (t2 when it is above minD, else t1), from the reference's own f64 a, b and the
+// correctly rounded square root, one division instead of two -- -1 = too close to call.  sphere_static returns
+// min(t1, t2) when both are >= minD, t1 / t2 when only that one is, which for a > 0 (t1 >= t2) is t2 when
+// t2 >= minD, else t1: the root sphere_any_f32 separated from minD by its margin.
+JSRT_HD int sphere_closest_f32(F3 o, F3 d, double minD, double lim, double &t_out) {
+    double te = 0;
+    bool second = false;
+    const int dec = sphere_any_f32(o, d, minD, lim, te, &second);
+    if (dec != 1) return dec;
+    const double a = dot3(d, d), b = dot3(d, o), c = dot3(o, o) - 1;
+    const double big = sqrt(b * b - a * c);  // (sphere_any_f32 decided: b * b - a * c >= 1e-30, a >= 1e-30)
+    t_out = second ? (-b - big) / a : (-b + big) / a;
+    return 1;
 }
 
 // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast.
@@ -1105,7 +1208,12 @@ __device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F
     const int k = P.gkind;
     double t = 0;
     if (k == JSRT_GEOM_AABB) {
+#ifdef JSRT_X_F32XF
+        const F3 lo = f3(XROWP(P.inv, o), XROWP(P.inv + 4, o), XROWP(P.inv + 8, o)),
+                 ld = f3(XROWD(P.inv, d), XROWD(P.inv + 4, d), XROWD(P.inv + 8, d));
+#else
         const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+#endif
         const int dec = box_any_f32(P.center, P.half, lo, box_ray(ld), minD, maxD, t);
         if (dec >= 0) return dec ? t : -DINF;
         return aabb_intersect(P.center, P.half, lo, ld, minD, maxD);
@@ -1125,6 +1233,33 @@ __device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F
     }
 #endif
     return prim_intersect<PF>(S, P, o, d, minD, maxD, transp, maxD);
+}
+
+// Primitive.intersect for a closest-hit cast (world.js:7-15): the caller keeps a distance only when
+// minD < t < lim (lim = min(maxD, the closest hit so far)), so for an AABB or Sphere geometry the f32 filters
+// above decide that first; an accepted distance comes back exact (one division, box_closest_f32 /
+// sphere_closest_f32), a rejected one as -Infinity, and only a decision too close to call runs the exact test.
+template <int PF, class PT>  // PT: DPrim in any address space
+__device__ __forceinline__ double prim_closest(const DScene &S, const PT &P, F3 o, F3 d, double minD, double maxD,
+                                               bool transp, double lim) {
+#if !defined(JSRT_NO_ANY_FILTER) && !defined(JSRT_NO_CLOSEST_FILTER)
+    if (!transp && !P.casts_shadow) return DINF;  // Primitive.intersect (as prim_intersect)
+    const int k = P.gkind;
+    double t = 0;
+    if (k == JSRT_GEOM_AABB) {
+        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+        const int dec = box_closest_f32(P.center, P.half, lo, ld, box_ray(ld), minD, lim, t);
+        if (dec >= 0) return dec ? t : -DINF;
+        return aabb_intersect(P.center, P.half, lo, ld, minD, maxD);
+    }
+    if (k == JSRT_GEOM_SPHERE) {
+        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+        const int dec = sphere_closest_f32(lo, ld, minD, lim, t);
+        if (dec >= 0) return dec ? t : -DINF;
+        return sphere_static(lo, ld, minD);
+    }
+#endif
+    return prim_intersect<PF>(S, P, o, d, minD, maxD, transp, lim);
 }
 
 // BVHAggregateNode.intersect with the BVH-local `ret` (aggregates.js:43-49, 207-225)
@@ -1281,7 +1416,7 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
             // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
             if (transp || R.p.casts_shadow) {
                 const double t = ANY ? prim_any<PF>(S, R.p, o, d, minD, maxD, transp)
-                                     : prim_intersect<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
+                                     : prim_closest<PF>(S, R.p, o, d, minD, maxD, transp, fmin(maxD, best.t));
                 if (t > minD && t < best.t && t < maxD) {
                     best = Hit{t, R.prim, 0};
                     flim = (float)best.t;

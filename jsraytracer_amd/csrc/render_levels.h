@@ -1120,6 +1120,9 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 &h0, co
     // (the light behind the surface, a black material, an edge-on area light) adds the same
     // nothing to colorFromLights' running sum (+0 + -0 = +0), so its shadow cast is skipped.
     if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return f3(0, 0, 0);
+#ifdef JSRT_X_NOCAST  // (timing experiment only) no shadow cast: every sample unshadowed
+    if (delta.x != 12345.0f) return c;
+#endif
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false, mask);
     if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
     return c;

@@ -79,6 +79,37 @@ extern "C" void tri_any(const float *verts, const float *rays, long n, double mi
     }
 }
 
+// closest-hit forms (World.cast's closest hit keeps minD < t < lim): exact[i] = 1 if the reference's distance
+// t_ref is accepted, tref[i] = t_ref; dec[i] = the filter's decision, tf[i] = its (exact) distance when 1
+extern "C" void box_closest(const float *boxes, const float *rays, const double *lims, long n, double minD, double maxD,
+                            int *exact, double *tref, int *dec, double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *b = boxes + 6 * i, *r = rays + 6 * i;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double lim = lims[i] < maxD ? lims[i] : maxD;
+        const double t = jsrt::aabb_intersect(b, b + 3, o, d, minD, maxD);
+        exact[i] = (t > minD && t < lim) ? 1 : 0;
+        tref[i] = t;
+        double e = 0;
+        dec[i] = jsrt::box_closest_f32(b, b + 3, o, d, jsrt::box_ray(d), minD, lim, e);
+        tf[i] = e;
+    }
+}
+extern "C" void sphere_closest(const float *rays, const double *lims, long n, double minD, double maxD, int *exact,
+                               double *tref, int *dec, double *tf) {
+    for (long i = 0; i < n; ++i) {
+        const float *r = rays + 6 * i;
+        const jsrt::F3 o = jsrt::f3(r[0], r[1], r[2]), d = jsrt::f3(r[3], r[4], r[5]);
+        const double lim = lims[i] < maxD ? lims[i] : maxD;
+        const double t = jsrt::sphere_static(o, d, minD);
+        exact[i] = (t > minD && t < lim) ? 1 : 0;
+        tref[i] = t;
+        double e = 0;
+        dec[i] = jsrt::sphere_closest_f32(o, d, minD, lim, e);
+        tf[i] = e;
+    }
+}
+
 // the spherePick stability test on the bits (device_common.h f32_stable_bits): out[i] = 1 if stable
 extern "C" void stable_bits(const double *d, long n, int *out) {
     for (long i = 0; i < n; ++i) out[i] = jsrt::f32_stable_bits(d[i]) ? 1 : 0;

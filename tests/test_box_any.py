@@ -287,3 +287,67 @@ def test_f32_stable_bits(lib):
     assert not (st & ~ref).any()
     assert (ref & ~st).mean() < 1e-4
     assert st.sum() > n // 2
+
+
+def _closest_lims(rng, tref, n):
+    """World.cast's closest-hit bound lim = min(maxD, the closest hit so far): random, +Infinity, and the exact
+    distance itself and its neighbours (a hit tied with the current closest one is not taken: t < lim)."""
+    lim = np.where(rng.random(n) < 0.3, np.inf, rng.uniform(0, 20, n))
+    fin = np.isfinite(tref) & (tref > 0)
+    pick = rng.integers(0, 5, n)
+    near = np.select([pick == 0, pick == 1, pick == 2, pick == 3],
+                     [tref, np.nextafter(tref, np.inf), np.nextafter(tref, -np.inf), tref * (1 + 1e-7)], tref * 2)
+    return np.where(fin & (rng.random(n) < 0.5), near, lim)
+
+
+def _check_closest(ex, tref, dec, tf, boundary, defer_max):
+    taken = dec >= 0
+    bad = np.flatnonzero(taken & (dec != ex))
+    assert len(bad) == 0, bad[:8]
+    acc = dec == 1
+    # an accepted distance is the reference's, bit for bit (the filter's one division is the exact one's)
+    assert np.array_equal(tf[acc].view(np.uint64), tref[acc].view(np.uint64)), np.flatnonzero(acc & (tf != tref))[:8]
+    assert ex.sum() > 1000 and (ex == 0).sum() > 1000
+    assert acc[~boundary].sum() > 0.99 * ex[~boundary].sum(), (acc[~boundary].sum(), ex[~boundary].sum())
+    assert (dec[~boundary] == -1).mean() < defer_max, (dec[~boundary] == -1).mean()
+
+
+@pytest.mark.parametrize("maxD", [1.0, np.inf])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_box_closest_decisions_and_distances_are_exact(lib, seed, maxD):
+    """box_closest_f32 (the closest-hit cast's AABB filter): its decisions are the exact acceptance minD < t < lim
+    and an accepted distance is AABB.intersect's own, bit for bit."""
+    import ctypes as C
+    lib.box_closest.argtypes = [C.c_void_p] * 3 + [C.c_long, C.c_double, C.c_double] + [C.c_void_p] * 4
+    boxes, rays, kind = _cases(seed)
+    n = len(boxes)
+    minD = 1e-4
+    # the exact distances first (lim = +inf), then lims placed around them
+    ex, tref, dec, tf = np.empty(n, np.int32), np.empty(n), np.empty(n, np.int32), np.empty(n)
+    lims = np.full(n, np.inf)
+    args = lambda lm: (boxes.ctypes.data, rays.ctypes.data, lm.ctypes.data, n, minD, maxD, ex.ctypes.data,
+                       tref.ctypes.data, dec.ctypes.data, tf.ctypes.data)
+    lib.box_closest(*args(lims))
+    lims = _closest_lims(np.random.default_rng(seed + 100), tref.copy(), n)
+    lib.box_closest(*args(lims))
+    tie = (lims == tref) | (lims == np.nextafter(tref, np.inf)) | (lims == np.nextafter(tref, -np.inf)) | (lims == tref * (1 + 1e-7))
+    _check_closest(ex, tref, dec, tf, (kind == 1) | (kind == 3) | (kind == 5) | tie, 1e-3)
+
+
+@pytest.mark.parametrize("maxD", [1.0, np.inf])
+@pytest.mark.parametrize("seed", [5, 6])
+def test_sphere_closest_decisions_and_distances_are_exact(lib, seed, maxD):
+    """sphere_closest_f32 (the closest-hit cast's Sphere filter), as test_box_closest for sphere_static."""
+    import ctypes as C
+    lib.sphere_closest.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_double, C.c_double] + [C.c_void_p] * 4
+    rays, boundary = _sphere_cases(seed)
+    n = len(rays)
+    ex, tref, dec, tf = np.empty(n, np.int32), np.empty(n), np.empty(n, np.int32), np.empty(n)
+    args = lambda lm: (rays.ctypes.data, lm.ctypes.data, n, 1e-4, maxD, ex.ctypes.data, tref.ctypes.data,
+                       dec.ctypes.data, tf.ctypes.data)
+    lims = np.full(n, np.inf)
+    lib.sphere_closest(*args(lims))
+    lims = _closest_lims(np.random.default_rng(seed + 100), tref.copy(), n)
+    lib.sphere_closest(*args(lims))
+    tie = (lims == tref) | (lims == np.nextafter(tref, np.inf)) | (lims == np.nextafter(tref, -np.inf)) | (lims == tref * (1 + 1e-7))
+    _check_closest(ex, tref, dec, tf, boundary | tie, 1e-3)
