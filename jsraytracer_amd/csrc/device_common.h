@@ -1239,24 +1239,29 @@ __device__ __forceinline__ double prim_any(const DScene &S, const PT &P, F3 o, F
 // minD < t < lim (lim = min(maxD, the closest hit so far)), so for an AABB or Sphere geometry the f32 filters
 // above decide that first; an accepted distance comes back exact (one division, box_closest_f32 /
 // sphere_closest_f32), a rejected one as -Infinity, and only a decision too close to call runs the exact test.
+// Not in the BVH profiles: there the top-level primitives are few and the filters' ~960 static instructions cost
+// the latency-bound mesh k_extend more than they save (bunny k_extend 25.4 -> 25.0 ms, dragon 3,804 -> 3,756 ms
+// without them, profiles/r05_s22_ab.txt)
 template <int PF, class PT>  // PT: DPrim in any address space
 __device__ __forceinline__ double prim_closest(const DScene &S, const PT &P, F3 o, F3 d, double minD, double maxD,
                                                bool transp, double lim) {
 #if !defined(JSRT_NO_ANY_FILTER) && !defined(JSRT_NO_CLOSEST_FILTER)
-    if (!transp && !P.casts_shadow) return DINF;  // Primitive.intersect (as prim_intersect)
-    const int k = P.gkind;
-    double t = 0;
-    if (k == JSRT_GEOM_AABB) {
-        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
-        const int dec = box_closest_f32(P.center, P.half, lo, ld, box_ray(ld), minD, lim, t);
-        if (dec >= 0) return dec ? t : -DINF;
-        return aabb_intersect(P.center, P.half, lo, ld, minD, maxD);
-    }
-    if (k == JSRT_GEOM_SPHERE) {
-        const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
-        const int dec = sphere_closest_f32(lo, ld, minD, lim, t);
-        if (dec >= 0) return dec ? t : -DINF;
-        return sphere_static(lo, ld, minD);
+    if constexpr (!(PF & PF_BVH)) {
+        if (!transp && !P.casts_shadow) return DINF;  // Primitive.intersect (as prim_intersect)
+        const int k = P.gkind;
+        double t = 0;
+        if (k == JSRT_GEOM_AABB) {
+            const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+            const int dec = box_closest_f32(P.center, P.half, lo, ld, box_ray(ld), minD, lim, t);
+            if (dec >= 0) return dec ? t : -DINF;
+            return aabb_intersect(P.center, P.half, lo, ld, minD, maxD);
+        }
+        if (k == JSRT_GEOM_SPHERE) {
+            const F3 lo = xf_point(P.inv, o), ld = xf_dir(P.inv, d);
+            const int dec = sphere_closest_f32(lo, ld, minD, lim, t);
+            if (dec >= 0) return dec ? t : -DINF;
+            return sphere_static(lo, ld, minD);
+        }
     }
 #endif
     return prim_intersect<PF>(S, P, o, d, minD, maxD, transp, lim);
