@@ -56,7 +56,7 @@ class FrameGather:
         [H, W] int32 (packed RGBA8) image on rank 0, None elsewhere."""
         import torch
         import torch.distributed as dist
-        if self.world > 1:
+        if self.world > 1 or dist.is_initialized():  # (a one-rank group still runs the collective)
             dist.gather(self.local, self.parts if self.rank == 0 else None, dst=0)
         else:
             self.parts = [self.local]
@@ -96,7 +96,7 @@ class AccumGather:
         accumulators on rank 0 (image order), None elsewhere."""
         import torch
         import torch.distributed as dist
-        if self.world > 1:
+        if self.world > 1 or dist.is_initialized():  # (a one-rank group still runs the collective)
             dist.gather(self.local, self.parts if self.rank == 0 else None, dst=0)
         else:
             self.parts = [self.local]

@@ -159,3 +159,49 @@ def test_gpu_accum_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
                                    accum=True)
     cols = list(range(37, W, 64))
     assert np.array_equal(acc[:, cols].view(np.uint32), ref[:, cols].view(np.uint32))
+
+
+def _rank_nccl_one(port, cb, outdir):
+    """One rank of a one-rank nccl (RCCL) group: its tile is the whole frame, and both gathers run RCCL's gather
+    on the device (the collective bench.py's N-GPU path runs over xGMI; one GPU is all this box has)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import jsraytracer_amd as jr
+    from jsraytracer_amd.tiles import AccumGather, FrameGather
+    from oracle import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    sc = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0)
+    fg = FrameGather(W, H, 0, 1, cb, device="cuda:0")
+    sc.render_device(fg.local.data_ptr(), col_block=cb, width=W, height=H, spp=SPP, max_depth=DEPTH, kind=1, seed=1,
+                     x_offset=0, x_delt=1, stats=False)
+    torch.cuda.synchronize()
+    img = fg.gather()
+    ag = AccumGather(W, H, 0, 1, cb, device="cuda:0")
+    sc.render_device_accum(ag.local.data_ptr(), col_block=cb, width=W, height=H, spp=SPP, max_depth=DEPTH, kind=1,
+                           seed=1, x_offset=0, x_delt=1)
+    torch.cuda.synchronize()
+    fin = AccumGather.finish(ag.gather(), 1, SPP)
+    torch.cuda.synchronize()
+    np.save(os.path.join(outdir, "composite.npy"), FrameGather.to_rgba8(img))
+    np.save(os.path.join(outdir, "composite_accum.npy"), FrameGather.to_rgba8(fin))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gpu_nccl_one_rank_gather(tmp_path):
+    """FrameGather / AccumGather through a real RCCL gather (nccl backend, one rank on device 0): the composite
+    equals the one-rank render bit for bit."""
+    import jsraytracer_amd as jr
+    from oracle import pyoracle
+    mp.start_processes(_rank_nccl_one, args=(_free_port(), 16, str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    full, _, _ = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0).render(W, H, SPP, DEPTH, 1, 1,
+                                                                                     want_colors=False)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "composite.npy")), full)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "composite_accum.npy")), full)
