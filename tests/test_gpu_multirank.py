@@ -161,7 +161,7 @@ def test_gpu_accum_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
     assert np.array_equal(acc[:, cols].view(np.uint32), ref[:, cols].view(np.uint32))
 
 
-def _rank_nccl_one(port, cb, outdir):
+def _rank_nccl_one(_i, port, cb, outdir):
     """One rank of a one-rank nccl (RCCL) group: its tile is the whole frame, and both gathers run RCCL's gather
     on the device (the collective bench.py's N-GPU path runs over xGMI; one GPU is all this box has)."""
     import sys
