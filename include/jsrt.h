@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define JSRT_ABI_VERSION 3
+#define JSRT_ABI_VERSION 4
 
 typedef struct jsrt_scene jsrt_scene;
 
@@ -53,8 +53,21 @@ typedef struct {
                                 | JSRT_EVENTS_ONE_STREAM: run the render on one stream, so that a launch's
                                 event interval is its own time (consecutive batches otherwise overlap on
                                 two streams). */
-    int32_t reserved[4];
+    int32_t mode;            /* JSRT_MODE_STRICT (0): the reference's numeric model, f64 scalars and f32 vectors
+                                (the only mode built; SURVEY §7's pure-f32 `fast` mode fails the 1e-5 bar on
+                                0.35-2.6 % of pixels and is refused: -1) */
+    uint32_t device_mask;    /* HIP devices that render this call's columns (bit d = device d; 0 = the scene's
+                                device).  jsrt_render only: the owned columns are interleaved over the k devices
+                                (device j takes x_offset + j * x_delt, step x_delt * k: the reference's own
+                                worker partition, renderers.js:88), each rendering from its own copy of the
+                                scene, and the host image is composited -- bit-identical to one device, as
+                                pixels never split.  Progress callbacks need a single device.  The device entry
+                                points accept only 0 or the scene's own device. */
+    int32_t reserved[2];
 } jsrt_params;
+
+#define JSRT_MODE_STRICT 0
+#define JSRT_MODE_FAST 1
 
 #define JSRT_EVENTS_ONE_STREAM ((int32_t)0x40000000)
 #define JSRT_STAGES 12

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JSRT_LIB") or os.path.join(HERE, "_build", "libjsrt.so")  # JSRT_LIB: A/B builds
-ABI_VERSION = 3  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
+ABI_VERSION = 4  # include/jsrt.h JSRT_ABI_VERSION: the Params / Stats layouts below
 EVENTS_ONE_STREAM = 0x40000000  # include/jsrt.h JSRT_EVENTS_ONE_STREAM (a Params.stage_events flag)
 
 
@@ -22,7 +22,8 @@ class Params(ctypes.Structure):
                 ("max_depth", ctypes.c_int32), ("kind", ctypes.c_int32), ("seed", ctypes.c_uint32),
                 ("x_offset", ctypes.c_int32), ("x_delt", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("samples_per_launch", ctypes.c_int32), ("timelimit_ms", ctypes.c_double),
-                ("max_paths", ctypes.c_int32), ("stage_events", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("max_paths", ctypes.c_int32), ("stage_events", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("device_mask", ctypes.c_uint32), ("reserved", ctypes.c_int32 * 2)]
 
 
 STAGES = ["k_gen", "k_extend", "k_shade", "k_shadow", "k_reduce", "k_accum", "k_final", "k_resolve", "spare8",

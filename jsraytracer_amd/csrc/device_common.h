@@ -1416,6 +1416,9 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         const auto &R = as_const(S.rootrec)[i];
         const bool need = live && root_needed(R.rb, o, ix, iy, iz, oabs, fminD, flim);
         if (!__any(need)) continue;
+#ifdef JSRT_X_CULLONLY  // (timing experiment only) any-hit casts run the culls but no test: nothing accepted
+        if (ANY) continue;
+#endif
         if (!need) {  // (a divergent if, not a divergent continue: the loop itself stays uniform)
         } else if (R.kind == INST_PRIM) {
             // Primitive.intersect: Infinity for a non-shadow-casting primitive in a shadow cast
@@ -1443,6 +1446,93 @@ __device__ __forceinline__ Hit world_cast(const DScene &S, F3 o, F3 d, double mi
         }
     }
     return best;
+}
+
+// The flat shadow loop (DScene::sroot): World.cast(P, delta, 1e-4, 1, false) as materials.js:250-252 reads it --
+// only whether some object accepts a hit in (minD, maxD) -- over the shadow-casting top-level Primitives of a
+// flat scene, grouped by geometry class.  Same culls and same any-hit tests (prim_any) as world_cast, so the
+// answer is the same bit for bit; only the visiting order differs, which an any-hit answer does not see.
+// What it saves is the generic loop's scalar bookkeeping: one root there is a chain of dependent scalar loads
+// and branches (bounded?, kind?, casts_shadow?, gkind?, then the matrix), each waited for on the wave's
+// critical path.  Here a record's 40 dwords arrive in three loads issued together and waited for once, the
+// class is a compile-time constant, and `mask` (over records, DScene::grid_smask) is walked by its set bits.
+// Returns true when some record accepts a hit (the lane's sample is shadowed).
+template <int C>
+__device__ __forceinline__ bool sroot_class(const DScene &S, uint64_t m, F3 o, F3 d, double minD, double maxD,
+                                            float ix, float iy, float iz, float oabs, bool &live) {
+    typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+    typedef uint32_t u8v __attribute__((ext_vector_type(8)));
+    const float fminD = (float)minD, flim = (float)maxD;
+    while (m) {
+        if (!__any(live)) break;
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        // the record in three loads issued together: [0, 16) inv 0..7, [16, 32) inv 8..11 + bounds, [32, 40)
+        const CONST_AS uint32_t *w = reinterpret_cast<const CONST_AS uint32_t *>(as_const(S.sroot) + j);
+        u16v a = *reinterpret_cast<const CONST_AS u16v *>(w);
+        u16v b = *reinterpret_cast<const CONST_AS u16v *>(w + 16);
+        u8v c = *reinterpret_cast<const CONST_AS u8v *>(w + 32);
+        __asm__ volatile("" : "+s"(a), "+s"(b), "+s"(c));  // all three in flight before the first use
+        double inv[12];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) inv[k] = __hiloint2double((int)a[2 * k + 1], (int)a[2 * k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) inv[8 + k] = __hiloint2double((int)b[2 * k + 1], (int)b[2 * k]);
+        RootBound rb;
+        rb.lo[0] = __uint_as_float(b[8]);
+        rb.lo[1] = __uint_as_float(b[9]);
+        rb.lo[2] = __uint_as_float(b[10]);
+        rb.k = __uint_as_float(b[11]);
+        rb.hi[0] = __uint_as_float(b[12]);
+        rb.hi[1] = __uint_as_float(b[13]);
+        rb.hi[2] = __uint_as_float(b[14]);
+        rb.e0 = __uint_as_float(b[15]);
+        rb.bounded = (int32_t)c[7];
+        const bool need = live && root_needed(rb, o, ix, iy, iz, oabs, fminD, flim);
+        if (!__any(need)) continue;
+        if (!need) continue;  // (a divergent if: the loop itself stays uniform)
+        double t = 0;
+        if constexpr (C == SR_BOX) {  // prim_any's AABB branch
+            const float ce[3] = {__uint_as_float(c[0]), __uint_as_float(c[1]), __uint_as_float(c[2])};
+            const float ha[3] = {__uint_as_float(c[4]), __uint_as_float(c[5]), __uint_as_float(c[6])};
+            const F3 lo = xf_point(inv, o), ld = xf_dir(inv, d);
+            const int dec = box_any_f32(ce, ha, lo, box_ray(ld), minD, maxD, t);
+            if (dec < 0) t = aabb_intersect(ce, ha, lo, ld, minD, maxD);
+            else if (!dec) t = -DINF;
+        } else if constexpr (C == SR_PLANE || C == SR_SQUARE || C == SR_CIRCLE) {  // prim_any's planar branch
+            const int k = C == SR_PLANE ? JSRT_GEOM_PLANE : C == SR_SQUARE ? JSRT_GEOM_SQUARE : JSRT_GEOM_CIRCLE;
+            const int dec = planar_any_f32(k, inv, o, d, minD, maxD, t);
+            if (dec < 0) t = planar_intersect(k, inv, o, d, minD, maxD);
+            else if (!dec) t = -DINF;
+        } else if constexpr (C == SR_SPHERE) {  // prim_any's Sphere branch
+            const F3 lo = xf_point(inv, o), ld = xf_dir(inv, d);
+            const int dec = sphere_any_f32(lo, ld, minD, maxD, t);
+            if (dec < 0) t = sphere_static(lo, ld, minD);
+            else if (!dec) t = -DINF;
+        } else {  // any other geometry: prim_any on the primitive itself
+            t = prim_any<PF_ANALYTIC>(S, S.prims[(int)c[3]], o, d, minD, maxD, false);
+        }
+        if (t > minD && t < maxD) live = false;  // accepted (world_cast: t > minD && t < best.t && t < maxD)
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool shadow_cast_flat(const DScene &S, F3 o, F3 d, double minD, double maxD, uint64_t m) {
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
+    const float oabs = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    bool live = true;
+    auto part = [&](int c) {  // the mask's bits of class c (records [sr_first[c], sr_first[c + 1]))
+        const int a = S.sr_first[c], b = S.sr_first[c + 1];
+        const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1), lo = a >= 64 ? ~0ull : ((1ull << a) - 1);
+        return m & hi & ~lo;
+    };
+    sroot_class<SR_BOX>(S, part(SR_BOX), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    sroot_class<SR_PLANE>(S, part(SR_PLANE), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    sroot_class<SR_SQUARE>(S, part(SR_SQUARE), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    sroot_class<SR_CIRCLE>(S, part(SR_CIRCLE), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    sroot_class<SR_SPHERE>(S, part(SR_SPHERE), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    sroot_class<SR_OTHER>(S, part(SR_OTHER), o, d, minD, maxD, ix, iy, iz, oabs, live);
+    return !live;
 }
 
 // --------------------------------------------------------------------------------------------

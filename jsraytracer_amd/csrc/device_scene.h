@@ -70,6 +70,24 @@ struct DRoot {           // one top-level object flattened for the world loop: e
 };
 static_assert(sizeof(DRoot) == 208, "DRoot");
 
+// One shadow-casting top-level Primitive as the flat shadow loop reads it (render_levels.h shadow_cast_flat):
+// every field the cull and the any-hit test read, in one 160-B record fetched by three scalar loads issued
+// together (DRoot spreads them over a 208-B record whose fields the generic loop loads one dependent branch
+// at a time).  The records are grouped by geometry class (SR_*), so the loop over a class runs one test
+// with no kind dispatch.  A shadow cast only asks whether SOME object accepts a hit in (1e-4, 1)
+// (materials.js:250-252, world.js:7-15), so any visiting order gives the same answer.
+enum : int32_t { SR_BOX, SR_PLANE, SR_SQUARE, SR_CIRCLE, SR_SPHERE, SR_OTHER, SR_N };
+struct SRoot {
+    double inv[12];      // the primitive's inv_transform rows 0..2 (DPrim::inv)
+    float lo[3], k;      // RootBound
+    float hi[3], e0;
+    float center[3];     // AABB geometry (DPrim::center / half)
+    int32_t prim;        // DPrim index
+    float half[3];
+    int32_t bounded;     // RootBound::bounded
+};
+static_assert(sizeof(SRoot) == 160, "SRoot");
+
 struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
     float cx, cy, cz;
     int32_t a;           // internal: lesser child; leaf: first index into leaf_prims[]
@@ -173,6 +191,13 @@ struct DScene {
     const void *stab;            // 16-B aligned
     int32_t stab_words, stab_words_shadow;
     int32_t stab_off[12];
+    // The flat shadow loop (all roots Primitives, at most 64; n_sroot = 0: not built): the shadow-casting roots
+    // as SRoot records grouped by class, class c at [sr_first[c], sr_first[c + 1]); grid_smask[b] = grid_mask[b]
+    // over these records (bit j: record j).
+    const SRoot *sroot;
+    const uint64_t *grid_smask;  // grid_cells + 1 entries
+    int32_t n_sroot, pad_sroot;
+    int32_t sr_first[SR_N + 1 + 1];
 };
 enum {  // DScene::stab tables, in image order: k_shadow's first (mat .. sample_light), then k_shade's
     STAB_MAT, STAB_MAT_FLAGS, STAB_MC, STAB_MC_CONST, STAB_SAMPLE_CALL, STAB_SAMPLE_LIGHT,

@@ -320,7 +320,9 @@ hipError_t Wavefront::reserve(size_t rays, size_t nodes, size_t hands, size_t pa
     // or after a frame that ran out of records (fix_all: the frame is redone with one record per ray slot)
     const char *fx = getenv("JSRT_FORCE_EXACT_PICK");
     const bool force_fix = fx && fx[0] == '1';
-    const size_t fixcap = (force_fix || fix_all) ? rays + 4096 : rays / 8 + 4096;
+    // (JSRT_FIX_CAP=n, a test knob: n records until a frame runs out, to exercise the redo on either pool)
+    const char *fc = getenv("JSRT_FIX_CAP");
+    const size_t fixcap = fix_all ? rays + 4096 : fc ? (size_t)std::max(0, atoi(fc)) : force_fix ? rays + 4096 : rays / 8 + 4096;
     bytes += need(3 * fixcap, 16) + need(64, 4);
     if (tree || hybrid)  // buckets
         bytes += need(MAX_TREE_DEPTH * BKT_LEVEL, 4) + need((hands / 256 + 1) * BKT_N, 4) + need(rays, 4);
@@ -652,7 +654,7 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         release_events();
         return e;
     }
-    bool conservative = false;
+    bool conservative = false, aborted = false;
     double reported = 0;  // completion already reported: a redone frame reports only beyond it
     for (int attempt = 0; e == hipSuccess; ++attempt) {
         if (kt) kt->attempts = (uint32_t)attempt + 1;
@@ -839,8 +841,9 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             }
         }
         if (e != hipSuccess) break;
-        if (stop) {  // an aborted frame is not redone (read_flags joins the side stream into st first)
+        if (stop) {  // an aborted frame is not redone (read_flags joins the side stream into st and waits for it)
             e = read_flags();
+            aborted = true;
             break;
         }
         // The frame flags of both pools, every schedule.  read_flags also joins the side stream into st, so the
@@ -852,8 +855,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
         if ((e = read_flags()) != hipSuccess) break;
         if (!flagged(LVL_FLAG) && !flagged(LVL_UNDER)) break;
         if (!learned) {  // chain: only k_shade's k_fix_dirs records can run out (fix_record)
-            if (wf.fix_all) { e = hipErrorOutOfMemory; break; }  // (never: a record per ray slot and level)
+            // both pools take a record per ray slot (the overflow may have been in either); the setting stays for
+            // later frames, like a doubled pool_factor.  A second overflow cannot happen: a level writes at most
+            // one record per ray slot
+            if (wf.fix_all && (!wf.twin || wf.twin->fix_all)) { e = hipErrorOutOfMemory; break; }
             wf.fix_all = true;
+            if (wf.twin) wf.twin->fix_all = true;
         } else if (flagged(LVL_FLAG)) {  // a batch outgrew the pool: twice the pool, relearn the counts
             if (paths * wf.pool_factor > ((size_t)1 << 31) * (hybrid ? 4 : 1)) { e = hipErrorOutOfMemory; break; }
             wf.pool_factor *= 2;
@@ -871,6 +878,9 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     if (h_lvl) (void)hipHostFree(h_lvl);
     release_events();
     if (e != hipSuccess) return e;
+    // an aborted frame leaves the caller's tile as the last preview left it (no k_final over a partial
+    // accumulator), with the device idle (read_flags waited): jsrt.h's -4 contract
+    if (aborted) return hipSuccess;
     if (!A.rgba) return hipSuccess;  // the caller takes the accumulator itself (jsrt_render_device_accum)
     const bool ev = kt && kt->on(KT_FINAL);
     if (ev) kt->ev[KT_FINAL].begin(st);

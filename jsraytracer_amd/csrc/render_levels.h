@@ -1111,7 +1111,8 @@ __device__ __forceinline__ F3 sample_unshadowed(const DScene &S, const float4 *h
     return sample_unshadowed<PF, SPH>(S, hp[0], hp[hs], hp, hs, s, P, delta);
 }
 
-template <int PF, bool SPH = true>
+// FLAT: the flat shadow loop (device_common.h shadow_cast_flat; `mask` is over DScene::sroot records)
+template <int PF, bool SPH = true, bool FLAT = false>
 __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 &h0, const float4 &h1, const float4 *hp,
                                            size_t hs, uint32_t s, uint64_t mask = ~0ull) {
     F3 P, delta;
@@ -1123,6 +1124,10 @@ __device__ __forceinline__ F3 sample_color(const DScene &S, const float4 &h0, co
 #ifdef JSRT_X_NOCAST  // (timing experiment only) no shadow cast: every sample unshadowed
     if (delta.x != 12345.0f) return c;
 #endif
+    if constexpr (FLAT) {
+        if (shadow_cast_flat(S, P, delta, 0.0001, 1, mask)) return f3(0, 0, 0);  // shadowed: contributes +0
+        return c;
+    }
     const Hit sh = world_cast<PF, true>(S, P, delta, 0.0001, 1, false, mask);
     if (shadowed(sh)) return f3(0, 0, 0);  // shadowed: contributes +0
     return c;
@@ -1150,7 +1155,8 @@ __device__ __forceinline__ F3 light_sums(const DScene &S, uint32_t G, F3 ret, F3
 // STAGE (flat scenes, DScene::stab; not SERIAL): k_shadow's tables (materials, colour constants, light-sample
 // indices) copied into LDS by every block behind its hand-off loads, so a sample's material -> colour chain is
 // LDS round trips
-template <int PF, bool CHAIN, bool SERIAL, bool SPH, bool STAGE = false>
+// FLAT (with STAGE; DScene::n_sroot > 0): the shadow casts through the flat shadow loop (shadow_cast_flat)
+template <int PF, bool CHAIN, bool SERIAL, bool SPH, bool STAGE = false, bool FLAT = false>
 __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSRT_SHADOW_OCC) SHADOW_ATTR void k_shadow(
     DScene S, WArgs W, int L) {
     const LevelRange R = CHAIN ? chain_level(W, L) : level_range(W, L);
@@ -1172,11 +1178,13 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSR
     // point in one grid cell -- the hand-off is bucketed by cell, so nearly every wave -- the world loop
     // visits only the roots a shadow segment from that cell can meet.
     uint64_t mask = ~0ull;
+    if (FLAT) mask = S.n_sroot >= 64 ? ~0ull : ((1ull << S.n_sroot) - 1);  // every record
     if (W.bucket && W.bucket_grid && S.grid_masked) {
         const uint64_t on = __ballot(in);
         if (on) {
             const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mi, __builtin_ctzll(on));
-            if (!__ballot(in && mi != m0) && m0 <= (uint32_t)S.grid_cells) mask = as_const(S.grid_mask)[m0];
+            if (!__ballot(in && mi != m0) && m0 <= (uint32_t)S.grid_cells)
+                mask = FLAT ? as_const(S.grid_smask)[m0] : as_const(S.grid_mask)[m0];
         }
     }
     if (CHAIN && !W.bucket && in) q = chain_slot(W, L, q);  // hand-off in level order: the chain's slot
@@ -1207,7 +1215,7 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADOW_OCC_FLAT : JSR
         __syncthreads();
         DScene SL = S;
         stab_bind(SL, stab_lds, false);
-        if (lit && s < ns) c = sample_color<PF, SPH>(SL, h0, h1, hp, W.hstride, s, mask);
+        if (lit && s < ns) c = sample_color<PF, SPH, FLAT>(SL, h0, h1, hp, W.hstride, s, mask);
     } else {
         if (lit && s < ns) c = sample_color<PF, SPH>(S, h0, h1, hp, W.hstride, s, mask);
     }
@@ -1441,7 +1449,11 @@ void run_batch(const DScene &S, const RenderArgs &A, const WArgs &W, hipStream_t
                 } else if (W.ns <= 1 || W.group > 1) {
                     const dim3 g(grid_ub(ub * (size_t)W.group));
                     const size_t sl = (size_t)S.stab_words_shadow * 16;  // the LDS-staged tables (flat scenes)
-                    if (PF == PF_ANALYTIC && sl && S.sphere_lights)
+                    if (PF == PF_ANALYTIC && sl && S.sphere_lights && S.n_sroot > 0)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true, PF == PF_ANALYTIC, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);
+                    else if (PF == PF_ANALYTIC && sl && S.n_sroot > 0)
+                        hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false, PF == PF_ANALYTIC, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);
+                    else if (PF == PF_ANALYTIC && sl && S.sphere_lights)
                         hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, true, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);
                     else if (PF == PF_ANALYTIC && sl)
                         hipLaunchKernelGGL((k_shadow<PF, CHAIN, false, false, PF == PF_ANALYTIC>), g, dim3(256), sl, st, S, W, L);

@@ -1063,6 +1063,7 @@ struct Loader {
             if (pc < 0 || S.sdf_insn[pc].op != SOP_FORM) S.sdf_all_forms = 0;
         }
         shadow_grid();
+        shadow_roots();
     }
 
     // Spatial buckets of the shadow hand-off and their shadow-root masks (DScene::grid_*).
@@ -1162,6 +1163,63 @@ struct Loader {
             S.grid_dim[k] = dim[k];
             S.grid_lo[k] = (float)lo[k];
             S.grid_inv[k] = (float)(dim[k] / ext[k]);
+        }
+    }
+
+    // The flat shadow loop's records (DScene::sroot): for a scene whose top level is at most 64 Primitives, the
+    // shadow-casting ones (a shadow cast is not transparent: Primitive.intersect gives Infinity for the others,
+    // world.js:104-113, which is never accepted) grouped by geometry class, and the grid masks remapped onto
+    // them.  Called after shadow_grid.
+    void shadow_roots() {
+        S.sroot.clear();
+        S.grid_smask.clear();
+        for (int c = 0; c < SR_N + 2; ++c) S.sr_first[c] = 0;
+        const size_t nr = S.roots.size();
+        if (!S.all_roots_prims || nr == 0 || nr > 64) return;
+        auto cls = [](int32_t g) {
+            switch (g) {
+            case JSRT_GEOM_AABB: return (int)SR_BOX;
+            case JSRT_GEOM_PLANE: return (int)SR_PLANE;
+            case JSRT_GEOM_SQUARE: return (int)SR_SQUARE;
+            case JSRT_GEOM_CIRCLE: return (int)SR_CIRCLE;
+            case JSRT_GEOM_SPHERE: return (int)SR_SPHERE;
+            default: return (int)SR_OTHER;
+            }
+        };
+        std::vector<int> perm;  // record j -> root index
+        for (int c = 0; c < SR_N; ++c) {
+            S.sr_first[c] = (int32_t)perm.size();
+            for (size_t r = 0; r < nr; ++r) {
+                const DPrim &P = S.prims[S.insts[S.roots[r]].prim];
+                if (P.casts_shadow && cls(P.gkind) == c) perm.push_back((int)r);
+            }
+        }
+        S.sr_first[SR_N] = S.sr_first[SR_N + 1] = (int32_t)perm.size();
+        for (int r : perm) {
+            const int32_t pi = S.insts[S.roots[r]].prim;
+            const DPrim &P = S.prims[pi];
+            const RootBound &rb = S.rbounds[r];
+            SRoot s;
+            memset(&s, 0, sizeof s);
+            memcpy(s.inv, P.inv, sizeof s.inv);
+            for (int k = 0; k < 3; ++k) {
+                s.lo[k] = rb.lo[k];
+                s.hi[k] = rb.hi[k];
+                s.center[k] = P.center[k];
+                s.half[k] = P.half[k];
+            }
+            s.k = rb.k;
+            s.e0 = rb.e0;
+            s.prim = pi;
+            s.bounded = rb.bounded;
+            S.sroot.push_back(s);
+        }
+        S.grid_smask.resize(S.grid_mask.size());
+        for (size_t b = 0; b < S.grid_mask.size(); ++b) {
+            uint64_t m = 0;
+            for (size_t j = 0; j < perm.size(); ++j)
+                if ((S.grid_mask[b] >> perm[j]) & 1ull) m |= 1ull << j;
+            S.grid_smask[b] = m;
         }
     }
 };

@@ -52,6 +52,10 @@ struct HostScene {
     std::vector<uint64_t> grid_mask;
     float grid_lo[3] = {0, 0, 0}, grid_inv[3] = {0, 0, 0};
     int32_t grid_dim[3] = {0, 0, 0}, grid_cells = 0;
+    // the flat shadow loop's records (DScene::sroot, empty: not built) and the grid masks over them
+    std::vector<SRoot> sroot;
+    std::vector<uint64_t> grid_smask;
+    int32_t sr_first[SR_N + 2] = {};
 };
 
 // Returns 0 on success; otherwise fills err.

@@ -20,7 +20,7 @@
  */
 const path = require("path");
 
-const ABI_VERSION = 3;  // include/jsrt.h JSRT_ABI_VERSION this wrapper is written against
+const ABI_VERSION = 4;  // include/jsrt.h JSRT_ABI_VERSION this wrapper is written against
 let _addon = null;
 function addon() {
     if (_addon) return _addon;
@@ -69,7 +69,8 @@ function readHeader(blob) {
 class HipRenderer {
     /*
      * scene: JSRT blob (Buffer / Uint8Array) or a live reference renderer object.
-     * opts:  {device = 0, seed = 1, samplesPerPixel, maxRecursionDepth, kind, width, height}
+     * opts:  {device = 0, seed = 1, samplesPerPixel, maxRecursionDepth, kind, width, height,
+     *         mode = "strict" (include/jsrt.h JSRT_MODE_*; "fast" is refused), deviceMask = 0 (jsrt_params)}
      *        (absent fields come from the scene's own renderer, as the reference's test.mjs sets them)
      */
     constructor(scene, opts = {}) {
@@ -84,6 +85,10 @@ class HipRenderer {
         this.maxRecursionDepth = opts.maxRecursionDepth !== undefined ? opts.maxRecursionDepth : h.maxDepth;
         this.seed = opts.seed !== undefined ? opts.seed : 1;
         this.device = opts.device || 0;
+        const MODES = { strict: 0, fast: 1 };
+        this.mode = opts.mode === undefined ? 0 : (typeof opts.mode === "string" ? MODES[opts.mode] : opts.mode);
+        if (this.mode === undefined) throw `HipRenderer: unknown numeric mode ${opts.mode}`;
+        this.deviceMask = opts.deviceMask || 0;
         this.handle = addon().sceneCreate(blob, this.device);
     }
     static computePixelCount(img, x_offset, x_delt) {  // renderers.js:7-9
@@ -98,7 +103,8 @@ class HipRenderer {
         return { width: img.width(), height: img.height(), samplesPerPixel: this.samplesPerPixel,
                  maxRecursionDepth: this.maxRecursionDepth, kind: this.kind, seed: this.seed,
                  x_offset, x_delt, device: this.device, timelimit: timelimit || 0,
-                 samplesPerLaunch: perPass ? (this.samplesPerLaunch || 1) : 0 };
+                 samplesPerLaunch: perPass ? (this.samplesPerLaunch || 1) : 0, mode: this.mode,
+                 deviceMask: this.deviceMask };
     }
     render(img, timelimit = 0, callback = false, x_offset = 0, x_delt = 1) {
         const p = this._params(img, timelimit, x_offset, x_delt, callback);

@@ -93,6 +93,8 @@ void read_params(napi_env env, napi_value o, jsrt_params *p) {
     p->timelimit_ms = prop_f64(env, o, "timelimit", 0);
     p->max_paths = prop_i32(env, o, "maxPaths", 0);
     p->samples_per_launch = prop_i32(env, o, "samplesPerLaunch", 0);
+    p->mode = prop_i32(env, o, "mode", JSRT_MODE_STRICT);
+    p->device_mask = (uint32_t)prop_f64(env, o, "deviceMask", 0);
 }
 
 napi_value stats_object(napi_env env, const jsrt_stats &st) {

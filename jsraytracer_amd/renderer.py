@@ -14,6 +14,19 @@ from . import _native
 from ._native import JsrtError, Params, Stats, check
 
 RENDERER_KINDS = {"SimpleRenderer": 0, "IncrementalMultisamplingRenderer": 1, "RandomMultisamplingRenderer": 2}
+MODE_STRICT, MODE_FAST = 0, 1  # include/jsrt.h JSRT_MODE_*: numeric modes; only strict is built
+MODES = {"strict": MODE_STRICT, "fast": MODE_FAST}
+
+
+def mode_code(mode):
+    """None / "strict" / "fast" / an int -> JSRT_MODE_* (the library refuses what it does not build)."""
+    if mode is None:
+        return MODE_STRICT
+    if isinstance(mode, str):
+        if mode not in MODES:
+            raise JsrtError(f"unknown numeric mode {mode!r}")
+        return MODES[mode]
+    return int(mode)
 
 
 class PixelBuffer:
@@ -100,16 +113,19 @@ class Scene:
 
     @staticmethod
     def params(width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1, device=0,
-               samples_per_launch=0, timelimit_ms=0.0, max_paths=0, stage_events=0):
+               samples_per_launch=0, timelimit_ms=0.0, max_paths=0, stage_events=0, mode=MODE_STRICT, device_mask=0):
         return Params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, device, samples_per_launch,
-                      timelimit_ms, max_paths, stage_events)
+                      timelimit_ms, max_paths, stage_events, mode, device_mask)
 
     def render(self, width=0, height=0, spp=0, max_depth=0, kind=-1, seed=1, x_offset=0, x_delt=1,
-               samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0, max_paths=0):
-        """Render into host arrays.  Returns (rgba u8[H,W,4], colors f32[H,W,4] or None, stats)."""
+               samples_per_launch=0, rgba=None, want_colors=True, progress=None, timelimit_ms=0.0, max_paths=0,
+               mode=None, device_mask=0):
+        """Render into host arrays.  Returns (rgba u8[H,W,4], colors f32[H,W,4] or None, stats).
+        mode: "strict" (the only numeric mode built; "fast" raises) or MODE_*; device_mask: bit d = HIP device d
+        renders part of the columns (jsrt.h jsrt_params::device_mask; 0 = the scene's device)."""
         L = _native.lib()
         p = self.params(width, height, spp, max_depth, kind, seed, x_offset, x_delt, self.device,
-                        samples_per_launch, timelimit_ms, max_paths)
+                        samples_per_launch, timelimit_ms, max_paths, mode=mode_code(mode), device_mask=device_mask)
         W = width if width > 0 else self.header()["width"]
         H = height if height > 0 else self.header()["height"]
         if rgba is None:
@@ -217,8 +233,10 @@ class HipRenderer:
     """Drop-in for SimpleRenderer / IncrementalMultisamplingRenderer / RandomMultisamplingRenderer
     (renderers.js).  ``scene`` is a Scene (or blob); kind/spp/depth default to the blob's renderer."""
 
-    def __init__(self, scene, samplesPerPixel=None, maxRecursionDepth=None, kind=None, seed=1, device=0):
+    def __init__(self, scene, samplesPerPixel=None, maxRecursionDepth=None, kind=None, seed=1, device=0, mode="strict",
+                 device_mask=0):
         self.scene = scene if isinstance(scene, Scene) else Scene(scene, device)
+        self.mode, self.device_mask = mode, device_mask  # jsrt_params::mode / device_mask
         hdr = self.scene.header()
         self.kind = hdr["kind"] if kind is None else (RENDERER_KINDS[kind] if isinstance(kind, str) else kind)
         self.samplesPerPixel = hdr["spp"] if samplesPerPixel is None else samplesPerPixel
@@ -244,5 +262,6 @@ class HipRenderer:
                 callback({"pass": p, "completion": c})
         self.scene.render(img.width(), img.height(), self.samplesPerPixel, self.maxRecursionDepth, self.kind,
                           self.seed, x_offset, x_delt, samples_per_launch=spl, rgba=img.imgdata, want_colors=False,
-                          progress=progress, timelimit_ms=float(timelimit or 0))
+                          progress=progress, timelimit_ms=float(timelimit or 0), mode=self.mode,
+                          device_mask=self.device_mask)
         return img

@@ -35,6 +35,21 @@ def column_permutation(width, world, col_block=1):
     return slot
 
 
+def _group_matches(world):
+    """True when this gatherer runs a collective: a process group is initialised.  Its size must be the
+    gatherer's world (a one-rank group still runs the collective, as the RCCL one-rank test does); a gatherer
+    built for another world size would gather over the whole default group with the wrong number of slots
+    and hang or fail, so that is refused here instead (advisor, round 5)."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        if world > 1:
+            raise RuntimeError(f"gather over {world} ranks needs an initialised process group")
+        return False
+    if dist.get_world_size() != world:
+        raise RuntimeError(f"gatherer built for {world} ranks in a process group of {dist.get_world_size()}")
+    return True
+
+
 class FrameGather:
     """Gathers per-rank [max_owned * H] u32 tiles to rank 0 and permutes them into an [H, W] image.
 
@@ -51,12 +66,15 @@ class FrameGather:
         self.slot = torch.as_tensor(column_permutation(width, world, col_block), device=device) if rank == 0 else None
         self.image = torch.empty((height, width), dtype=torch.int32, device=device) if rank == 0 else None
 
+    def _collective(self):
+        return _group_matches(self.world)
+
     def gather(self):
         """Collective: every rank calls it after its tile is rendered into self.local.  Returns the
         [H, W] int32 (packed RGBA8) image on rank 0, None elsewhere."""
         import torch
         import torch.distributed as dist
-        if self.world > 1 or dist.is_initialized():  # (a one-rank group still runs the collective)
+        if self._collective():
             dist.gather(self.local, self.parts if self.rank == 0 else None, dst=0)
         else:
             self.parts = [self.local]
@@ -91,12 +109,15 @@ class AccumGather:
         self.slot = torch.as_tensor(column_permutation(width, world, col_block), device=device) if rank == 0 else None
         self.image = torch.empty((height, width, 4), dtype=torch.float32, device=device) if rank == 0 else None
 
+    def _collective(self):
+        return _group_matches(self.world)
+
     def gather(self):
         """Collective: every rank calls it after its accumulator tile is in self.local.  Returns the [H, W, 4] f32
         accumulators on rank 0 (image order), None elsewhere."""
         import torch
         import torch.distributed as dist
-        if self.world > 1 or dist.is_initialized():  # (a one-rank group still runs the collective)
+        if self._collective():
             dist.gather(self.local, self.parts if self.rank == 0 else None, dst=0)
         else:
             self.parts = [self.local]
@@ -142,6 +163,11 @@ def render_progressive(scene, fg, dev_tile, on_preview, timelimit_ms=0.0, host_t
 
     import torch
     import torch.distributed as dist
+    if kw.get("kind", 1) != 1:
+        # the running-mean previews are the Incremental renderer's (renderers.js:70-117); Simple / Random report
+        # per batch, and a rank that owns no column has no batches to report, so the ranks' per-callback
+        # collectives could not stay in step (advisor, round 5)
+        raise ValueError("render_progressive renders the Incremental kind (kind=1) only")
     last = [time.perf_counter()]
     dev = "cpu" if host_tiles or fg.world == 1 else dev_tile.device
     status = torch.zeros(4, dtype=torch.int32, device=dev)  # unclean, failed, due, done: max over ranks

@@ -48,7 +48,7 @@ def test_library_is_gfx950(lib):
 
 
 def test_abi_version_and_helpers(lib):
-    assert lib.jsrt_abi_version() == 3
+    assert lib.jsrt_abi_version() == 4
     from jsraytracer_amd import owned_columns
     assert owned_columns(10, 0, 1) == 10
     assert owned_columns(10, 1, 3) == 3            # 1, 4, 7
@@ -118,3 +118,19 @@ def test_bench_exits_nonzero_on_parity_failure():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "--ab" in r.stderr and not r.stdout
+
+
+def test_params_layout_and_mode_names():
+    """jsrt_params (ABI 4): mode and device_mask take two of round 5's four reserved words, so the struct keeps its
+    size; the host's mode names map to JSRT_MODE_* and an unknown name is refused before any call."""
+    import ctypes
+
+    import jsraytracer_amd as jr
+    from jsraytracer_amd import _native
+    from jsraytracer_amd.renderer import MODE_FAST, MODE_STRICT, mode_code
+    P = _native.Params
+    assert ctypes.sizeof(P) == 72
+    assert P.mode.offset == 56 and P.device_mask.offset == 60 and P.reserved.offset == 64
+    assert (mode_code(None), mode_code("strict"), mode_code("fast"), mode_code(1)) == (MODE_STRICT, MODE_STRICT, MODE_FAST, 1)
+    with pytest.raises(jr.JsrtError):
+        mode_code("turbo")

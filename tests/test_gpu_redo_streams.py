@@ -25,7 +25,11 @@ CASES = [  # scene, schedule it runs on, W, H, spp, max_paths (several batches -
     ("refraction_path", "hybrid", 40, 40, 3, 1600),
     ("bunny_path", "tree", 40, 32, 3, 1280),
 ]
-KNOBS = [{}, {"JSRT_POOL_FACTOR": "1"}, {"JSRT_BOUND_MARGIN": "0.5"}]
+# JSRT_FIX_CAP=0 with every diffuse pick through k_fix_dirs (JSRT_FORCE_EXACT_PICK=1): the chain schedule's fix
+# records run out on both pools, and the frame is redone with a record per ray slot on both (advisor, round 5:
+# the redo used to enlarge only the first pool's records, so an overflow in a twin-pool batch failed again)
+FIXCAP = {"JSRT_FIX_CAP": "0", "JSRT_FORCE_EXACT_PICK": "1"}
+KNOBS = [{}, {"JSRT_POOL_FACTOR": "1"}, {"JSRT_BOUND_MARGIN": "0.5"}, FIXCAP]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: "+".join(f"{a}={b}" for a, b in k.items()) or "default")
@@ -34,8 +38,10 @@ def test_device_frame_complete_on_return(monkeypatch, case, knobs):
     torch = pytest.importorskip("torch")
     import jsraytracer_amd as jr
     name, sched, W, H, spp, max_paths = case
-    if sched == "chain" and knobs:
+    if sched == "chain" and knobs and knobs is not FIXCAP:
         pytest.skip("the chain schedule has no learned pool or bounds")
+    if sched != "chain" and knobs is FIXCAP:
+        pytest.skip("fix-record redo: the chain schedule's (learned schedules grow their records with the pool)")
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     blob = pyoracle.golden_scene(name)
@@ -57,5 +63,5 @@ def test_device_frame_complete_on_return(monkeypatch, case, knobs):
     # the same frame on a fresh scene, with stats: it ran as several batches, and the knob took the redo path
     st = jr.Scene(blob, device=0).render_device(tile.data_ptr(), stream_ptr=stream.cuda_stream, **kw)
     assert st["batches"] >= 3
-    if knobs.get("JSRT_BOUND_MARGIN") or (knobs.get("JSRT_POOL_FACTOR") and sched == "tree"):
+    if knobs.get("JSRT_BOUND_MARGIN") or (knobs.get("JSRT_POOL_FACTOR") and sched == "tree") or knobs is FIXCAP:
         assert st["attempts"] >= 2

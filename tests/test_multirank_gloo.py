@@ -221,3 +221,39 @@ def test_gloo_accum_gather_is_the_single_process_accumulator(tmp_path, world, cb
     got = np.load(os.path.join(tmp_path, "accum.npy"))
     _, _, _, ref = pyoracle.render(pyoracle.golden_scene("cornell_box_path"), W, H, spp, 8, 1, 5, threads=1, accum=True)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _mismatch_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from jsraytracer_amd.tiles import AccumGather, FrameGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    errs = []
+    for cls in (FrameGather, AccumGather):
+        g = cls(8, 4, 0, 1)  # a one-rank gatherer inside a two-rank group
+        try:
+            g.gather()
+        except RuntimeError as e:
+            errs.append(str(e))
+    with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+        f.write("\n".join(errs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gatherer_refuses_a_group_of_another_size(tmp_path):
+    """A one-rank FrameGather / AccumGather in a process whose default group has two ranks must refuse to gather
+    (a gather over the whole group with one slot would hang or fail; advisor, round 5), on every rank."""
+    mp.start_processes(_mismatch_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        errs = open(os.path.join(tmp_path, f"err{r}.txt")).read().splitlines()
+        assert len(errs) == 2 and all("built for 1 ranks in a process group of 2" in e for e in errs)
+
+
+def test_progressive_refuses_non_incremental_kinds():
+    """render_progressive is the Incremental renderer's running-mean preview (renderers.js:70-117); the Simple
+    and Random kinds report per batch, which a rank owning no column cannot match (advisor, round 5)."""
+    from jsraytracer_amd.tiles import render_progressive
+    for kind in (0, 2):
+        with pytest.raises(ValueError, match="Incremental"):
+            render_progressive(None, None, None, None, kind=kind)

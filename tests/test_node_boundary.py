@@ -43,7 +43,7 @@ def test_addon_exports(addon):
     keys, nums = r.stdout.strip().split("\n")
     assert json.loads(keys) == sorted(["sceneCreate", "sceneDestroy", "renderSync", "render", "deviceCount",
                                        "abiVersion", "ownedColumns", "attachObj", "blobFromJson"])
-    assert nums.split() == ["3", "16", "3"]
+    assert nums.split() == ["4", "16", "3"]
 
 
 def test_addon_attach_obj_matches_python_and_reference(addon, tmp_path):
@@ -184,7 +184,7 @@ def test_node_wrapper_checks_abi_version(addon, tmp_path):
     r = subprocess.run([NODE, "-e", code], capture_output=True, text=True, timeout=60, cwd=ROOT,
                        env=dict(os.environ, JSRT_NODE_ADDON=str(stub)))
     assert r.returncode == 0, r.stderr
-    assert r.stdout.startswith("HipRenderer: libjsrt ABI 1, expected 3")
+    assert r.stdout.startswith("HipRenderer: libjsrt ABI 1, expected 4")
 
 
 @pytest.mark.gpu
