@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--stages", action="store_true", help="per share, one more render on one stream with HIP events "
+                    "around every launch: its per-stage ms (where a share's time goes) and batch count")
+    ap.add_argument("--only-rank0", action="store_true", help="time rank 0's share only at N > 1 (a quicker stage split)")
     args = ap.parse_args()
     import torch
 
@@ -42,7 +45,7 @@ def main():
     for n in [int(x) for x in args.ranks.split(",")]:
         cb = 16 if n > 1 else 1
         shares = []
-        for r in range(n):
+        for r in range(1 if (args.only_rank0 and n > 1) else n):
             sc = jr.Scene(blob, device=0)  # each rank's own scene (its own learned pools and bounds)
             ncols = len(owned_px(W, r, n, cb))
             tile = torch.zeros(max(ncols, 1) * H, dtype=torch.int32, device="cuda:0")
@@ -55,10 +58,19 @@ def main():
                 sc.render_device(tile.data_ptr(), **kw)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / args.steps * 1e3
-            shares.append({"rank": r, "columns": ncols, "paths": ncols * H * spp, "ms": ms})
+            share = {"rank": r, "columns": ncols, "paths": ncols * H * spp, "ms": ms}
+            if args.stages:
+                st = sc.render_device(tile.data_ptr(), **dict(kw, stats=True, stage_events=jr._native.EVENTS_ONE_STREAM))
+                share["stages_ms"] = {k: round(v, 3) for k, v in st["stage_ms"].items() if v}
+                share["batches"], share["attempts"] = st["batches"], st["attempts"]
+                print(f"   stages {share['stages_ms']} batches {st['batches']} attempts {st['attempts']}", file=sys.stderr,
+                      flush=True)
+            shares.append(share)
             sc.close()
             print(f"N={n} rank {r}: {ncols} columns, {ms:.2f} ms", file=sys.stderr, flush=True)
         worst = max(s["ms"] for s in shares)
+        if len(shares) < n:  # --only-rank0: rank 0's share stands for every share
+            shares += [dict(shares[0], rank=r, projected_from_rank0=True) for r in range(1, n)]
         if n == 1:
             t1 = worst
         row = {"n": n, "max_share_ms": worst, "mean_share_ms": sum(s["ms"] for s in shares) / n,
