@@ -100,6 +100,8 @@ struct WArgs {
     int32_t bucket;    // tree schedule: 0, or 1 + shift: k_shadow reads lit nodes bucketed by hit primitive >> shift (bkt)
     int32_t child_sort; // tree schedule: k_shade appends a block's children grouped by direction octant
     int32_t bucket_grid; // bucketed hand-off keyed by the hit point's grid cell (DScene::grid_*), not the primitive
+    int32_t pixel_major; // path q of the batch: pixel q / nsb, sample q % nsb (a pixel's samples side by side);
+                         // else sample q / npix, pixel q % npix (render.hip k_gen / k_accum / k_resolve)
     size_t pool, level_cap;
     size_t nstride, hstride;  // plane strides of child / slot and of hand
     size_t sstride;           // entries of sray / scol (0: persistent casts not used)

@@ -27,8 +27,9 @@
 #ifndef JSRT_SHADOW_OCC
 #define JSRT_SHADOW_OCC 6
 #endif
-#ifndef JSRT_SHADOW_OCC_FLAT  // analytic profile: 7 waves (72 VGPRs, no spill) once k_shadow carries no sphere-light code
-#define JSRT_SHADOW_OCC_FLAT 7
+#ifndef JSRT_SHADOW_OCC_FLAT  // analytic profile: 8 waves (64 VGPRs, 15 spilled): cornell k_shadow 41.9 -> 41.5 ms and
+// every interleaved 8-step pair faster (round 6, profiles/r06_s5_ab.txt); 7 waves (72 VGPRs) before
+#define JSRT_SHADOW_OCC_FLAT 8
 #endif
 #ifndef JSRT_EXTEND_OCC
 #define JSRT_EXTEND_OCC 5

@@ -29,7 +29,9 @@ CASES = [  # scene, schedule it runs on, W, H, spp, max_paths (several batches -
 # records run out on both pools, and the frame is redone with a record per ray slot on both (advisor, round 5:
 # the redo used to enlarge only the first pool's records, so an overflow in a twin-pool batch failed again)
 FIXCAP = {"JSRT_FIX_CAP": "0", "JSRT_FORCE_EXACT_PICK": "1"}
-KNOBS = [{}, {"JSRT_POOL_FACTOR": "1"}, {"JSRT_BOUND_MARGIN": "0.5"}, FIXCAP]
+# both orders of a batch's paths (WArgs::pixel_major): a pixel's samples side by side, or sample by sample
+KNOBS = [{}, {"JSRT_POOL_FACTOR": "1"}, {"JSRT_BOUND_MARGIN": "0.5"}, FIXCAP, {"JSRT_PIXEL_MAJOR": "1"},
+         {"JSRT_PIXEL_MAJOR": "0"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: "+".join(f"{a}={b}" for a, b in k.items()) or "default")
@@ -38,7 +40,7 @@ def test_device_frame_complete_on_return(monkeypatch, case, knobs):
     torch = pytest.importorskip("torch")
     import jsraytracer_amd as jr
     name, sched, W, H, spp, max_paths = case
-    if sched == "chain" and knobs and knobs is not FIXCAP:
+    if sched == "chain" and knobs and knobs is not FIXCAP and "JSRT_PIXEL_MAJOR" not in knobs:
         pytest.skip("the chain schedule has no learned pool or bounds")
     if sched != "chain" and knobs is FIXCAP:
         pytest.skip("fix-record redo: the chain schedule's (learned schedules grow their records with the pool)")

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--stages", action="store_true", help="per share, one more render on one stream with HIP events "
                     "around every launch: its per-stage ms (where a share's time goes) and batch count")
+    ap.add_argument("--col-block", type=int, default=16, help="columns per block dealt round-robin to ranks (bench.py "
+                    "--col-block; W / N: one contiguous strip per rank)")
     ap.add_argument("--only-rank0", action="store_true", help="time rank 0's share only at N > 1 (a quicker stage split)")
     args = ap.parse_args()
     import torch
@@ -43,7 +45,7 @@ def main():
     rows = []
     t1 = None
     for n in [int(x) for x in args.ranks.split(",")]:
-        cb = 16 if n > 1 else 1
+        cb = (args.col_block if args.col_block > 0 else W // n) if n > 1 else 1
         shares = []
         for r in range(1 if (args.only_rank0 and n > 1) else n):
             sc = jr.Scene(blob, device=0)  # each rank's own scene (its own learned pools and bounds)
@@ -77,6 +79,7 @@ def main():
                "projected_samples_per_s": W * H * spp / (worst * 1e-3),
                "efficiency_vs_1": (t1 / (n * worst)) if t1 else None,
                "gather_bytes": W * H * 4 if n > 1 else 0, "shares": shares}
+        row["col_block"] = cb
         rows.append(row)
         print(json.dumps({k: v for k, v in row.items() if k != "shares"}), flush=True)
     out = {"config": args.config, "workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}", "steps": args.steps,
