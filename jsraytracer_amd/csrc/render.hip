@@ -536,6 +536,9 @@ void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStrea
 }
 }  // namespace
 
+#ifndef SPLIT_PIXELS_DEFAULT
+#define SPLIT_PIXELS_DEFAULT true  // bunny 656.6 -> 687.2 M/s (profiles/r06_s9_bunny.txt)
+#endif
 hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront &wf, hipStream_t st, KernelTimes *kt,
                         size_t max_paths, const std::function<bool(int, double, bool)> &progress,
                         const std::function<bool()> &due) {
@@ -558,18 +561,19 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     else nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)A.spp));
     if (A.samples_per_batch > 0) nsb = std::min<uint32_t>(nsb, (uint32_t)A.samples_per_batch);
     // Pixel-major batches (round 6; the BVH and SDF profiles, WArgs::pixel_major): a pixel's samples are side by
-    // side in the batch, and a batch holds up to JSRT_BATCH_SPP (16) samples of fewer pixels rather than a few
-    // samples of every pixel.  The rays in flight (~0.5 M) then come from a small patch of the image, so their
+    // side in the batch, and a batch holds every sample of its pixels (up to JSRT_BATCH_SPP = 256) rather than a
+    // few samples of every pixel.  The rays in flight (~0.5 M) then come from a small patch of the image, so their
     // casts walk a small part of the BVH and keep it in the caches.  The keyed RNG and the per-pixel
-    // accumulation in sample order leave the image unchanged.  Measured (profiles/r06_s6_ab_pixel_major_*.txt):
-    // bunny 556 -> 657 M/s, the dragon 798 -> 889 (its N = 8 shares, whose batches already held 16 samples of
-    // a share's pixels, 768 -> 493 ms); the flat hybrid chain loses (cornell k_accum's strided reads), so it keeps
-    // the sample-major order.  JSRT_PIXEL_MAJOR=0/1: A/B.
+    // accumulation in sample order leave the image unchanged.  Measured (profiles/r06_s6_ab_pixel_major_*.txt,
+    // r06_s7_dragon.txt, r06_s8_dragon.txt): bunny 556 -> 657 M/s, SDF_Menger 148 -> 160, the dragon 798 -> 889 in
+    // pixel-major order alone, then 1,116 / 1,228 / 1,306 / 1,416 / 1,475 / 1,533 M/s at 8 / 16 / 32 / 64 / 128 /
+    // 256 samples per batch; the flat hybrid chain loses (cornell k_accum's strided reads), so it keeps the
+    // sample-major order.  JSRT_PIXEL_MAJOR=0/1: A/B.
     const char *pm = getenv("JSRT_PIXEL_MAJOR");
     const bool pixel_major = pm ? pm[0] == '1' : S.profile != PF_ANALYTIC;
     if (pixel_major) {
         const char *bs = getenv("JSRT_BATCH_SPP");
-        uint32_t want = (uint32_t)(bs ? std::max(1, atoi(bs)) : 16);
+        uint32_t want = (uint32_t)(bs ? std::max(1, atoi(bs)) : 256);
         want = std::min<uint32_t>(want, (uint32_t)A.spp);
         if (A.samples_per_batch > 0) want = std::min<uint32_t>(want, (uint32_t)A.samples_per_batch);
         if (nsb < want) {  // fewer pixels, more of their samples
@@ -588,9 +592,15 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
     // JSRT_SPLIT_FRAME=0 keeps one batch; JSRT_SPLIT_MIN=k (A/B) splits from 2^k paths.
     const char *sf = getenv("JSRT_SPLIT_FRAME"), *sm = getenv("JSRT_SPLIT_MIN");  // (A/B: log2 of the paths)
     const int split_min = sm ? std::max(1, std::min(40, atoi(sm))) : 22;
+    // (Pixel-major batches split their pixels instead -- two halves of the image, every sample each -- so that the
+    // rays in flight keep coming from few pixels; JSRT_SPLIT_PIXELS=0/1: A/B.)
+    const char *spx = getenv("JSRT_SPLIT_PIXELS");
+    const bool split_pixels = pixel_major && (spx ? spx[0] == '1' : SPLIT_PIXELS_DEFAULT);
     if (!persist && !(sf && sf[0] == '0') && npix == npix_total && nsb == (uint32_t)A.spp && A.spp >= 2 &&
-        (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << split_min))
-        nsb = (uint32_t)((A.spp + 1) / 2);  // odd spp: halves of (spp + 1) / 2 and (spp - 1) / 2 samples
+        (uint64_t)npix * (uint64_t)A.spp >= ((uint64_t)1 << split_min)) {
+        if (split_pixels && npix_total >= 128) npix = ((npix_total / 2) + 63) & ~63u;  // whole patches: 64-pixel units
+        else nsb = (uint32_t)((A.spp + 1) / 2);  // odd spp: halves of (spp + 1) / 2 and (spp - 1) / 2 samples
+    }
     // Chain schedule when no node can have two children: depth x paths node records, nothing can
     // overflow, batches are enqueued back to back.  Tree schedule otherwise: a ray pool for all
     // levels of a batch (one level may hold half of it), compacted level by level.  Its launches
