@@ -1319,19 +1319,8 @@ __device__ __forceinline__ Hit bvh_cast(const DScene &S, const DInst &I, F3 o, F
                     }
                 }
             } else {
-                // closest hit: greater child first, the reference's order (aggregates.js:221-222), whose pruning on
-                // the running closest hit decides ties and rounding-edge cases.  A shadow cast (ANY) only asks
-                // whether some accepted hit exists, and before its first one nothing is pruned, so any order gives
-                // its answer: the child nearer along the split axis first, which reaches an occluder sooner.
-                const int lesser = (int)((uint32_t)N.a & BVH_CHILD_MASK);
-                bool greater_first = true;
-                if (ANY && S.bvh_near_first) {
-                    const uint32_t ax = ((uint32_t)N.a >> 29) & 3u;
-                    const float dax = ax == 0 ? d.x : (ax == 1 ? d.y : d.z);
-                    greater_first = (dax > 0.0f) != (N.a < 0);
-                }
-                stack[sp * stride] = greater_first ? lesser : N.b;  // visited after the other subtree
-                stack[(sp + 1) * stride] = greater_first ? N.b : lesser;
+                stack[sp * stride] = N.a;  // lesser, visited after the greater subtree
+                stack[(sp + 1) * stride] = N.b;
                 sp += 2;
             }
         }

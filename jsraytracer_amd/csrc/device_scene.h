@@ -88,13 +88,9 @@ struct SRoot {
 };
 static_assert(sizeof(SRoot) == 160, "SRoot");
 
-// An internal node's `a`: the lesser child (bits 0..28), the axis separating its children (bits 29..30) and whether
-// the greater child lies on that axis's positive side (bit 31) -- the shadow casts' near-child-first order
-constexpr uint32_t BVH_CHILD_MASK = 0x1FFFFFFFu;
 struct DBvhNode {        // aggregates.js:187-202 BVHAggregateNode
     float cx, cy, cz;
-    int32_t a;           // internal: lesser child | split axis << 29 | greater-on-positive-side << 31;
-                         // leaf: first index into leaf_prims[]
+    int32_t a;           // internal: lesser child; leaf: first index into leaf_prims[]
     float hx, hy, hz;
     int32_t b;           // internal: greater child (>= 0); leaf: ~count (< 0)
 };
@@ -200,8 +196,6 @@ struct DScene {
     // over these records (bit j: record j).
     const SRoot *sroot;
     const uint64_t *grid_smask;  // grid_cells + 1 entries
-    int32_t bvh_near_first;      // shadow casts walk the nearer BVH child first (DBvhNode::a; JSRT_BVH_NEAR=0: A/B)
-    int32_t pad_near;
     int32_t n_sroot, pad_sroot;
     int32_t sr_first[SR_N + 1 + 1];
 };

@@ -749,17 +749,28 @@ __global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_EXTEND_OCC_FLAT : JSR
         const bool lit = hp >= 0 && S.prim_lit[hp] != 0;
         const int lane = (int)__lane_id();
         const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        // one LDS atomic per distinct bucket of the wave (a few hot buckets would serialise), issued by the bucket's
+        // first lane: the loop only finds each lane's leader and rank (no memory operation in it), then the leaders'
+        // atomics go out as ONE instruction to distinct addresses and each lane reads its leader's base (round 6:
+        // the loop had waited for one atomic's return per distinct bucket, ~25 per wave of scattered hits)
         uint64_t todo = __ballot(lit);
-        while (todo) {  // one LDS atomic per distinct bucket of the wave (a few hot buckets would serialise)
+        int leader = lane;
+        uint32_t rk = 0, cnt = 0;
+        while (todo) {
             const int first = __builtin_ctzll(todo);
-            const int bv = __shfl(b, first);
+            const int bv = __builtin_amdgcn_readlane(b, first);
             const uint64_t m = __ballot(lit && b == bv);
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(&hist[bv], (uint32_t)__popcll(m));
-            base = __shfl(base, first);
-            if (lit && b == bv) W.brank[i] = ((uint32_t)bv << 16) | (base + (uint32_t)__popcll(m & lt));
+            if (lit && b == bv) {
+                leader = first;
+                rk = (uint32_t)__popcll(m & lt);
+            }
+            if (lane == first) cnt = (uint32_t)__popcll(m);
             todo &= ~m;
         }
+        uint32_t base = 0;
+        if (lit && lane == leader) base = atomicAdd(&hist[b], cnt);
+        base = (uint32_t)__shfl((int)base, leader);
+        if (lit) W.brank[i] = ((uint32_t)b << 16) | (base + rk);
         __threadfence_block();
         uint32_t done = 0;
         if (lane == 0) done = atomicAdd(&waves_done, 1u);

@@ -390,23 +390,8 @@ struct Loader {
                 }
             }
         } else {
-            if (R.lesser < 0 || (uint32_t)R.lesser >= B.n_bvh || R.greater < 0 || (uint32_t)R.greater >= B.n_bvh)
-                fail("BVH node index out of range");
-            // the children's separation axis and side, for the shadow casts' near-child-first order (device_common.h
-            // bvh_cast): the axis along which the greater child's centre is farthest from the lesser's
-            const jsrt_rec_bvhnode &Lr = B.bvh[R.lesser], &Gr = B.bvh[R.greater];
-            int axis = 0;
-            double sep = -1;
-            for (int k = 0; k < 3; ++k)
-                if (fabs((double)Gr.center[k] - Lr.center[k]) > sep) {
-                    sep = fabs((double)Gr.center[k] - Lr.center[k]);
-                    axis = k;
-                }
-            const bool gpos = (double)Gr.center[axis] - Lr.center[axis] > 0;
             d.a = bvh_node(R.lesser, depth + 1, fast);
             d.b = bvh_node(R.greater, depth + 1, fast);
-            if ((uint32_t)d.a >= BVH_CHILD_MASK) fail("BVH too large (2^29 nodes)");
-            d.a = (int32_t)((uint32_t)d.a | ((uint32_t)axis << 29) | (gpos ? 0x80000000u : 0u));
         }
         S.bvh[idx] = d;
         return idx;
