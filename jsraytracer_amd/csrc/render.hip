@@ -536,6 +536,9 @@ void run_batch_pf(const DScene &S, const RenderArgs &A, const WArgs &W, hipStrea
 }
 }  // namespace
 
+#ifndef TILE_PATCHES_DEFAULT
+#define TILE_PATCHES_DEFAULT 8
+#endif
 #ifndef SPLIT_PIXELS_DEFAULT
 #define SPLIT_PIXELS_DEFAULT true  // bunny 656.6 -> 687.2 M/s (profiles/r06_s9_bunny.txt)
 #endif
@@ -580,6 +583,12 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
             npix = (uint32_t)std::min<size_t>(npix_total, std::max<size_t>(64, (max_paths / want) & ~(size_t)63));
             nsb = (uint32_t)std::max<size_t>(1, std::min<size_t>(max_paths / npix, (size_t)want));
         }
+    }
+    // ... and their pixels in compact tiles of JSRT_TILE_PATCHES x JSRT_TILE_PATCHES 8 x 8 patches (pixel_of)
+    RenderArgs At = A;
+    {
+        const char *tp = getenv("JSRT_TILE_PATCHES");
+        At.tile_p = pixel_major ? (tp ? std::max(0, atoi(tp)) : TILE_PATCHES_DEFAULT) : 0;
     }
     // persistent casts: SDF scenes whose top level is primitives only (JSRT_PERSIST=0 disables)
     const char *pe = getenv("JSRT_PERSIST");
@@ -824,8 +833,8 @@ hipError_t render_frame(const DScene &S, const RenderArgs &A, int ns, Wavefront 
                     sync.shade_done = pw.ev_shade;
                     sync.shadow_done = pw.ev_shadow;
                 }
-                if (chain) run_batch_pf<true>(S, A, Wb, sb, kt, bound, &sync);
-                else run_batch_pf<false>(S, A, Wb, sb, kt, bound, &sync);
+                if (chain) run_batch_pf<true>(S, At, Wb, sb, kt, bound, &sync);
+                else run_batch_pf<false>(S, At, Wb, sb, kt, bound, &sync);
                 if ((e = hipGetLastError()) != hipSuccess) break;
                 done += (uint64_t)Wb.npix * nb;
                 if (kt) ++kt->batches;

@@ -31,6 +31,7 @@ struct RenderArgs {
     int32_t patches_x; // ceil(ncols / 8)
     int32_t patches;   // patches_x * ceil(H / 8)
     int32_t samples_per_batch;  // progress granularity: cap on samples per batch (<= 0: none)
+    int32_t tile_p;    // > 0: pixel order of the batches in tiles of tile_p x tile_p patches (render_levels.h pixel_of)
 };
 
 // node info bits (k_shade -> k_shadow / k_reduce / k_resolve)

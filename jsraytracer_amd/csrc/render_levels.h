@@ -210,9 +210,21 @@ __device__ __forceinline__ void write_result(const WArgs &W, uint32_t i, F3 c) {
     }
 }
 
-// patch-ordered owned pixel index -> (owned column c, row py, image column px)
+// patch-ordered owned pixel index -> (owned column c, row py, image column px).  8 x 8-pixel patches in raster order,
+// or (A.tile_p > 0) in raster order within tiles of tile_p x tile_p patches taken in raster order, the last tile
+// row and column partial: the pixels of consecutive indices, and so the rays a batch has in flight, then cover a
+// compact region of the image rather than a band as wide as it (the BVH working set of their casts)
 __device__ __forceinline__ bool pixel_of(const RenderArgs &A, uint32_t p, int &c, int &py, int &px) {
-    const int patch = (int)(p >> 6), lane = (int)(p & 63);
+    int patch = (int)(p >> 6);
+    const int lane = (int)(p & 63);
+    if (A.tile_p > 0) {
+        const int T = A.tile_p, pxn = A.patches_x, pyn = A.patches / A.patches_x;
+        const int ty = patch / (pxn * T), r = patch - ty * pxn * T;  // (every tile row but the last is full)
+        const int h = min(T, pyn - ty * T);
+        const int tx = r / (T * h), r2 = r - tx * T * h;  // (every tile of the row but the last is full)
+        const int w = min(T, pxn - tx * T);
+        patch = (ty * T + r2 / w) * pxn + tx * T + r2 % w;
+    }
     c = (patch % A.patches_x) * 8 + (lane & 7);
     py = (patch / A.patches_x) * 8 + (lane >> 3);
     if (c >= A.ncols || py >= A.H) return false;

@@ -30,8 +30,10 @@ CASES = [  # scene, schedule it runs on, W, H, spp, max_paths (several batches -
 # the redo used to enlarge only the first pool's records, so an overflow in a twin-pool batch failed again)
 FIXCAP = {"JSRT_FIX_CAP": "0", "JSRT_FORCE_EXACT_PICK": "1"}
 # both orders of a batch's paths (WArgs::pixel_major): a pixel's samples side by side, or sample by sample
+# and the pixel-major batches' tile order (pixel_of) with partial tiles at the image edges
 KNOBS = [{}, {"JSRT_POOL_FACTOR": "1"}, {"JSRT_BOUND_MARGIN": "0.5"}, FIXCAP, {"JSRT_PIXEL_MAJOR": "1"},
-         {"JSRT_PIXEL_MAJOR": "0"}]
+         {"JSRT_PIXEL_MAJOR": "0"}, {"JSRT_PIXEL_MAJOR": "1", "JSRT_TILE_PATCHES": "2"},
+         {"JSRT_PIXEL_MAJOR": "1", "JSRT_TILE_PATCHES": "3", "JSRT_BATCH_SPP": "2"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: "+".join(f"{a}={b}" for a, b in k.items()) or "default")
