@@ -91,6 +91,11 @@ __host__ __device__ inline double pow10_exact(int k) {
     return r;
 }
 
+#ifdef JSRT_TP8_TABLE  // (A/B) the powers from a per-lane load of a constant table
+static __constant__ double p10_table[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                            1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+#endif
+
 // Fast path for 1e-37 <= |v| < 1e8 (every value the reference scenes produce).  The product
 // x * 10^k is carried as p + err: for k <= 22 one fma gives the exact rounding error; for k in
 // 23..44 it is x * 1e22 * 10^(k-22) in double-double (err then carries ~2^-100 relative error,
@@ -160,10 +165,11 @@ __host__ __device__ inline double to_precision8(double v) {
 // to_precision8 without branches for 1e-15 <= |v| < 1e8 (the SDF repetition range and every checkerboard
 // value), the same IEEE operations as the fast path above: the decade estimate e10 from the binary exponent
 // is floor(log10 |v|) or one less, so the scaled value of the estimate and of the decade above are both
-// formed and the one in [1e7, 1e8] kept (the fast path's loop, unrolled); the parse multiplies by 10^max(k2,
-// 0) (exact: n * 10 < 2^53) and divides by 10^max(-k2, 0) (a division by 1 is exact), one IEEE division
-// either way.  Per lane this is straight-line code: no divergent branches, whose exec-mask bookkeeping made
-// the SDF march SALU-heavy.  Bit-identical to to_precision8 (tests/test_js_number.py).
+// formed and the one in [1e7, 1e8] kept (the fast path's loop, unrolled); the parse is one IEEE division by
+// the kept power of ten (a division by 1 is exact), and that power is the only one formed per call (round 6:
+// the parse's own two powers and the second scaled power cost SDF_Menger 16 %, profiles/r06_s14_tp8_menger.txt).
+// Per lane this is straight-line code: no divergent branches, whose exec-mask bookkeeping made the SDF march
+// SALU-heavy.  Bit-identical to to_precision8 (tests/test_js_number.py).
 __host__ __device__ inline double to_precision8_sl(double v) {
     const double x = fabs(v);
     int ex;
@@ -171,20 +177,23 @@ __host__ __device__ inline double to_precision8_sl(double v) {
     const int e10 = (int)floor((double)(ex - 1) * 0.30102999566398120);
     if (!(x >= 1e-15 && x < 1e8) || e10 < -15) return to_precision8(v);  // (also 0, NaN, +-inf)
     const int kA = 7 - e10;  // 0..22 for e10 in [-15, 7]
-    const double PA = pow10_exact(kA), PB = pow10_exact(kA > 0 ? kA - 1 : 0);
+    // 10^(kA - 1) and 10^kA = 10 * 10^(kA - 1), both exact (5^22 < 2^53)
+#if defined(JSRT_TP8_TABLE) && defined(__HIP_DEVICE_COMPILE__)
+    const double PB = p10_table[kA > 0 ? kA - 1 : 0], PA = kA > 0 ? PB * 10.0 : 1.0;
+#else
+    const double PB = pow10_exact(kA > 0 ? kA - 1 : 0), PA = kA > 0 ? PB * 10.0 : 1.0;
+#endif
     const double pA = x * PA, errA = fma(x, PA, -pA);
     // the estimate was a decade low when the scaled value reaches 1e8 (the fast path's second iteration)
     const bool hi = kA > 0 && (pA > 1e8 || (pA == 1e8 && errA >= 0));
     const double pB = x * PB, errB = fma(x, PB, -pB);
     const double p = hi ? pB : pA, err = hi ? errB : errA;
-    int e = hi ? e10 + 1 : e10;
     const double r = floor(p), fr = p - r;
-    double n = r + ((fr > 0.5 || (fr == 0.5 && err >= 0)) ? 1.0 : 0.0);
-    const bool carry = n == 1e8;
-    n = carry ? 1e7 : n;
-    e += carry ? 1 : 0;
-    const int k2 = e - 7;
-    const double res = (n * pow10_exact(k2 > 0 ? k2 : 0)) / pow10_exact(k2 < 0 ? -k2 : 0);
+    const double n = r + ((fr > 0.5 || (fr == 0.5 && err >= 0)) ? 1.0 : 0.0);
+    // the parse n * 10^(e - 7), e <= 7: one IEEE division by 10^(7 - e), the power already formed (PA or PB).  A
+    // carry (n == 1e8, the 8 digits 1e7 of the next decade) keeps n = 1e8 and the divisor: 1e8 / 10^m and
+    // 1e7 / 10^(m - 1) (or 1e7 * 10 at m = 0) are correctly rounded values of the same real number.
+    const double res = n / (hi ? PB : PA);
     return v < 0 ? -res : res;
 }
 

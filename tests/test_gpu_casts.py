@@ -52,3 +52,29 @@ def test_gpu_cast_dragon_against_oracle(jr):
             np.testing.assert_array_equal(obj, oe)
     finally:
         scene.close()
+
+
+def test_gpu_cast_menger_inside_against_oracle(jr):
+    """SDF_Menger's march from points inside and around the sponge (its holes at every level), against the
+    oracle: the sponge form's early exit (sdf_forms.h sdf_form_runion; JSRT_SDF_EXIT=0 turns it off) must give
+    every distance bit for bit.  The sponge is Mat4.translation([-3.5, 0.5, -3.5]) x rotationY(-0.15) of a
+    unit box (tests/SDF_Menger/test.mjs)."""
+    blob = pyoracle.golden_scene("SDF_Menger")
+    rng = np.random.default_rng(11)
+    c = np.array([-3.5, 0.5, -3.5])
+    o = (c + rng.uniform(-1.3, 1.3, (8192, 3))).astype(np.float32)
+    d = rng.normal(size=(8192, 3))
+    d[: 2048] = np.round(d[: 2048] * 2) / 2 + 1e-3  # near axis-aligned: long marches along the hole walls
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    rays = np.concatenate([o, d], 1)
+    scene = jr.Scene(blob, device=0)
+    try:
+        for minD, maxD, tr, rr in ((0.0001, float("inf"), True, rays),
+                                   (0.0001, 1.0, False, np.concatenate([o, (np.roll(o, 1, 0) - o)], 1))):
+            t, obj = scene.cast(rr, minD, maxD, tr)
+            te, oe = pyoracle.cast(blob, rr, minD, maxD, tr)
+            assert np.isfinite(te).sum() > 1000
+            np.testing.assert_array_equal(t.view(np.uint64), te.view(np.uint64))
+            np.testing.assert_array_equal(obj, oe)
+    finally:
+        scene.close()
