@@ -666,6 +666,38 @@ JSRT_HD double sdf_minbox(const T *k, int n, F3 P) {
     return nan ? __builtin_nan("") : r;
 }
 
+// sdf_minbox of the Menger sponge's cross (MINBOX pad 1: the host matched three boxes, box i infinite along axis
+// i, every other half size the same f32 h; tests/SDF_Menger/test.mjs:27-36), bit for bit.  For finite P the bars
+// share q_i = |p_i| - h (or0 changes nothing: no NaN, and a zero difference of two non-negative values is +0),
+// and a bar's infinite axis has q = -inf: max(q, 0) = +0 and js_maxf(-inf, v) = js_maxf(v, -inf) = v.  So bar x
+// has a = |m|^2 = fma(mz, mz, my^2) (dot3 with a zero term: fma(0, 0, c) = c for c >= +0; the squares of f32
+// values are exact) and c = min(max(qy, qz), 0), and likewise y, z -- one subtraction, one max0 and one square
+// per axis instead of per box and axis.  No -0 or NaN arises, so the plain comparisons are Math.max / min.  A
+// non-finite P (|p| - inf is NaN there) takes sdf_minbox.
+template <class T>
+JSRT_HD double sdf_cross(const T *k, F3 P) {
+    if (!(fabsf(P.x) <= __FLT_MAX__ && fabsf(P.y) <= __FLT_MAX__ && fabsf(P.z) <= __FLT_MAX__)) return sdf_minbox(k, 3, P);
+    const float h = (float)k[1];
+    const float qx = fabsf(P.x) - h, qy = fabsf(P.y) - h, qz = fabsf(P.z) - h;
+    const double mx = qx > 0.0f ? qx : 0.0f, my = qy > 0.0f ? qy : 0.0f, mz = qz > 0.0f ? qz : 0.0f;
+    const double sx = mx * mx, sy = my * my;
+    const double a[3] = {fma(mz, mz, sy), fma(mz, mz, sx), fma(mx, mx, sy)};
+    const float c[3] = {qy > qz ? qy : qz, qx > qz ? qx : qz, qx > qy ? qx : qy};
+    double amin = __builtin_inf(), din = 0.0;
+    bool inside = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (a[i] == 0.0) {
+            const double d = 0.0 + (double)(c[i] > 0.0f ? 0.0f : c[i]);
+            din = inside ? (d < din ? d : din) : d;
+            inside = true;
+        } else {
+            amin = a[i] < amin ? a[i] : amin;
+        }
+    }
+    return inside ? din : sqrt(amin);
+}
+
 // SDFInfiniteRepetitionTransformer.transform (sdf.js:471-473): Math.fmod(p + s/2, s) - s/2 per axis.
 // k[3..5]: 1/s when s is a power of two (x / s and x * (1 / s) are then the same rounding of the
 // same real number), else 0.
@@ -779,8 +811,8 @@ __device__ __forceinline__ double sdf_run(const DScene &S, int pc, int end, F3 P
             break;
         }
         case SOP_XREP: P = sdf_xrep(K + ia, P); break;
-        case SOP_MINBOX:  // BOX x ib, MIN ib
-            dst.set(dsp++, sdf_minbox(K + ia, ib, P));
+        case SOP_MINBOX:  // BOX x ib, MIN ib (pad 1: the Menger cross)
+            dst.set(dsp++, uni(code[pc].pad) ? sdf_cross(K + ia, P) : sdf_minbox(K + ia, ib, P));
             break;
         case SOP_XMATS:  // TPUSH XMAT TPOP_MUL
             P = xf_point(K + ia, P);

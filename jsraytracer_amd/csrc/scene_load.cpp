@@ -3,6 +3,7 @@
 // here (shading contexts, area-light normals) round exactly as the reference's JS does.
 #include "scene_load.h"
 
+#include <float.h>
 #include <math.h>
 #include <string.h>
 
@@ -567,6 +568,22 @@ struct Loader {
             fail("SDF tree too deep/wide for the GPU program stacks");
     }
 
+    // A union of n boxes at sdf_const[a] (4 doubles apart) that is the Menger sponge's cross (device_common.h
+    // sdf_cross): three boxes, box i infinite along axis i, its other half sizes and those of the other boxes the
+    // same finite, non-negative f32 h.  JSRT_SDF_CROSS=0 leaves every union to sdf_minbox (A/B).
+    bool is_cross(int32_t a, size_t n) const {
+        const char *knob = getenv("JSRT_SDF_CROSS");
+        if (n != 3 || (knob && knob[0] == '0')) return false;
+        const float h = (float)S.sdf_const.at(a + 1);
+        if (!(h >= 0.0f && h <= FLT_MAX)) return false;
+        for (int b = 0; b < 3; ++b)
+            for (int i = 0; i < 3; ++i) {
+                const double v = S.sdf_const.at(a + 4 * b + i);
+                if (i == b ? !(v == INFINITY) : (float)v != h) return false;
+            }
+        return true;
+    }
+
     // Peephole fusion of a compiled range into one-dispatch forms (sdf_program.h); returns the fused
     // range appended to the program.  Every fused op performs the same IEEE operations in the same
     // order as the sequence it replaces; only scale multiplies by an exact 1.0 (a transformer that
@@ -602,7 +619,7 @@ struct Loader {
                     size_t n = 1;
                     while (op(i + n) == SOP_BOX && in[i + n].a == in[i].a + 4 * (int32_t)n) ++n;
                     if (n >= 2 && op(i + n) == SOP_MIN && in[i + n].a == (int32_t)n) {
-                        out.push_back(SdfInsn{SOP_MINBOX, in[i].a, (int32_t)n, 0}), og.push_back(-1);
+                        out.push_back(SdfInsn{SOP_MINBOX, in[i].a, (int32_t)n, is_cross(in[i].a, n) ? 1 : 0}), og.push_back(-1);
                         i += n + 1, changed = true;
                         continue;
                     }

@@ -12,11 +12,11 @@
 // SFORM_RUNION: RecursiveTransformUnion(Union(Box x n), Sequence(Matrix, Repetition), iterations)
 // (sdf.js:349-357), the Menger sponge's hole pattern.  Fused program (pc: after the SOP_FORM marker):
 //   [0] PUSHP
-//   [1] MINBOX a, b        d1 = Union(boxes)(P)                             sdf.js:83-85
+//   [1] MINBOX a, b, x     d1 = Union(boxes)(P)  (x: the Menger cross)     sdf.js:83-85
 //   [2] TPUSH              s = 1
 //   [3] LOOP a             iterations
 //   [4] XMATREP a, b, pad    Q = rep(M Q), s = s * (1 * (1 * k))            sdf.js:387-394, 433-435, 471-473
-//   [5] MINBOX a, b          d = Union(boxes)(Q)
+//   [5] MINBOX a, b, x       d = Union(boxes)(Q)
 //   [6] MULSMIN              d1 = min(d1, d * s)                           sdf.js:354-356
 //   [7] ENDLOOP  [8] TPOP  [9] POPP
 template <class KT, class CT>
@@ -25,13 +25,14 @@ __device__ __forceinline__ double sdf_form_runion(const KT *K, const CT *code, i
     const int iters = uni(code[pc + 3].a);
     const int xm = uni(code[pc + 4].a), xs = uni(code[pc + 4].b), xr = uni(code[pc + 4].pad);
     const int u1 = uni(code[pc + 5].a), un1 = uni(code[pc + 5].b);
-    double d1 = sdf_minbox(K + u0, un0, P);
+    const bool x0 = uni(code[pc + 1].pad) != 0, x1 = uni(code[pc + 5].pad) != 0;  // the Menger cross (sdf_cross)
+    double d1 = x0 ? sdf_cross(K + u0, P) : sdf_minbox(K + u0, un0, P);
     double s = 1.0;
     F3 Q = P;
     for (int it = 0; it < iters; ++it) {
         Q = sdf_xrep(K + xr, xf_point(K + xm, Q));
         s = s * (1.0 * (1.0 * K[xs]));
-        const double d = sdf_minbox(K + u1, un1, Q);
+        const double d = x1 ? sdf_cross(K + u1, Q) : sdf_minbox(K + u1, un1, Q);
         d1 = js_min(d1, d * s);
     }
     return d1;

@@ -1,5 +1,6 @@
 // Exhaustive check behind a candidate fast path of toPrecision(8)'s parse (js_number.h to_precision8,
-// DESIGN.md §8): for every 8-digit integer n in [1e7, 1e8) and m in 1..22, the quotient through the
+// DESIGN.md §8): for every 8-digit integer n in [1e7, 1e8) and m in 0..22,
+// and n = 1e8 (to_precision8_sl's carry keeps it), the quotient through the
 // correctly rounded reciprocal R = RN(10^-m) and one fma correction of its remainder,
 //     q0 = RN(n * R), q = RN(q0 + RN(n - q0 * 10^m) * R)   (the remainder term exact by fma),
 // equals the IEEE quotient RN(n / 10^m).  Prints the mismatches per m (all 0).
@@ -13,9 +14,9 @@ int main(void) {
                                  1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
     long bad[23] = {0};
     #pragma omp parallel for schedule(dynamic)
-    for (int m = 1; m <= 22; ++m) {
+    for (int m = 0; m <= 22; ++m) {
         long b = 0;
-        for (int64_t n = 10000000; n < 100000000; ++n) {
+        for (int64_t n = 10000000; n <= 100000000; ++n) {
             const double x = (double)n;
             const double q0 = x * R[m];
             const double rem = fma(-q0, P[m], x);
@@ -24,6 +25,6 @@ int main(void) {
         }
         bad[m] = b;
     }
-    for (int m = 1; m <= 22; ++m) printf("m=%d bad=%ld\n", m, bad[m]);
+    for (int m = 0; m <= 22; ++m) printf("m=%d bad=%ld\n", m, bad[m]);
     return 0;
 }

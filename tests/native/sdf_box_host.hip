@@ -12,3 +12,12 @@ extern "C" void box_union(const double *boxes, int n, const float *pts, long m, 
         out[j] = jsrt::sdf_minbox(boxes, n, P);
     }
 }
+
+// the Menger cross (sdf_cross, boxes: 3 x 4 doubles as the host matched them) against sdf_minbox
+extern "C" void cross_union(const double *boxes, const float *pts, long m, double *out_ref, double *out) {
+    for (long j = 0; j < m; ++j) {
+        const jsrt::F3 P = jsrt::f3(pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]);
+        out_ref[j] = jsrt::sdf_minbox(boxes, 3, P);
+        out[j] = jsrt::sdf_cross(boxes, P);
+    }
+}

@@ -60,6 +60,11 @@ def test_gpu_rank_tiles_gather_to_single_rank_frame(tmp_path, world, cb):
     full, _, _ = jr.Scene(pyoracle.golden_scene("cornell_box_path"), device=0).render(W, H, SPP, DEPTH, 1, 1,
                                                                                      want_colors=False)
     assert np.array_equal(comp, full)
+    # and the composite's columns of every rank against the oracle (not only HIP against HIP)
+    _, ref, _ = pyoracle.render(pyoracle.golden_scene("cornell_box_path"), W, H, SPP, DEPTH, 1, 1, 5, 41)
+    cols = list(range(5, W, 41))
+    assert len({(c // cb) % world for c in cols}) == world
+    assert np.array_equal(comp.reshape(H, W, 4)[:, cols], ref[:, cols])
 
 
 PSPP = 4  # progressive frame: passes 0..PSPP-2 call back, the last pass is the final frame

@@ -24,8 +24,8 @@ def lib():
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(f) for f in [SRC] + HDRS):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-                        "-fno-fast-math", "-fPIC", "-shared", SRC, "-o", OUT + ".tmp"], check=True)
-        os.replace(OUT + ".tmp", OUT)
+                        "-fno-fast-math", "-fPIC", "-shared", SRC, "-o", OUT + f".{os.getpid()}.tmp"], check=True)
+        os.replace(OUT + f".{os.getpid()}.tmp", OUT)
     L = ctypes.CDLL(OUT)
     L.pow_dd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p]
     return L

@@ -19,11 +19,12 @@ def lib():
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(f) for f in [SRC] + HDRS):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-                        "-fno-fast-math", "-fPIC", "-shared", SRC, "-o", OUT + ".tmp"], check=True)
-        os.replace(OUT + ".tmp", OUT)
+                        "-fno-fast-math", "-fPIC", "-shared", SRC, "-o", OUT + f".{os.getpid()}.tmp"], check=True)
+        os.replace(OUT + f".{os.getpid()}.tmp", OUT)
     L = ctypes.CDLL(OUT)
     L.box_union.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p,
                             ctypes.c_void_p]
+    L.cross_union.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
     return L
 
 
@@ -47,3 +48,25 @@ def test_minbox_equals_reference_union(lib, n):
         ref, got = _run(lib, boxes, np.concatenate(pts))
         same = (ref.view(np.uint64) == got.view(np.uint64)) | (np.isnan(ref) & np.isnan(got))
         assert same.all(), f"{int((~same).sum())} differ"
+
+
+@pytest.mark.parametrize("h", [1 / 3, 1.0, 0.0, 1e-30])
+def test_cross_equals_minbox(lib, h):
+    """sdf_cross (the Menger cross: box i infinite along axis i, half size h across) is bit-identical to the
+    generic union on points everywhere, on the bars' faces, edges and corners, at +-0, and at non-finite
+    coordinates (which it hands to sdf_minbox)."""
+    rng = np.random.default_rng(int(h * 1000) + 3)
+    boxes = np.full((3, 4), h)
+    boxes[:, 3] = 0
+    boxes[[0, 1, 2], [0, 1, 2]] = np.inf
+    hf = np.float32(h)
+    edge = np.array([0.0, -0.0, hf, -hf, np.nextafter(hf, np.float32(1)), np.nextafter(hf, np.float32(0))], np.float32)
+    pts = [rng.uniform(-3, 3, (300_000, 3)), rng.uniform(-1.2 * h - 1e-6, 1.2 * h + 1e-6, (300_000, 3)),
+           rng.choice(edge, (100_000, 3)),
+           np.c_[rng.choice(edge, 100_000), rng.uniform(-2, 2, (100_000, 2))][:, rng.permutation(3)],
+           np.array([[np.nan, 0, 0], [0, np.nan, 1], [np.inf, 0, 0], [-np.inf, 1, 1], [0, 0, np.inf], [3e38, 0, 0]])]
+    pts = np.ascontiguousarray(np.concatenate(pts), np.float32)
+    ref, got = np.empty(len(pts)), np.empty(len(pts))
+    lib.cross_union(np.ascontiguousarray(boxes).ctypes.data, pts.ctypes.data, len(pts), ref.ctypes.data, got.ctypes.data)
+    same = (ref.view(np.uint64) == got.view(np.uint64)) | (np.isnan(ref) & np.isnan(got))
+    assert same.all(), f"{int((~same).sum())} differ, e.g. {pts[~same][:3].tolist()}"
