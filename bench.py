@@ -224,8 +224,9 @@ def load_rocprof(config, kname, build_id):
         if m.get("build_id") != build_id or m.get("config") != config:
             continue
         k = _stage_kernel(m["kernels"], kname, lambda c: c["calls"] * c["avg_ms"])
-        if k:
-            return os.path.relpath(meta, ROOT), k, m["kernels"][k]["avg_ms"]
+        if k:  # the instrumented step's launches (tools/stamp_stats.py) are the ones the live figure times
+            c = m["kernels"][k]
+            return os.path.relpath(meta, ROOT), k, c.get("instrumented_step", c)["avg_ms"], c["avg_ms"]
     return None
 
 
@@ -250,7 +251,8 @@ def roofline(config, bound, dom, avg_ms, launches, counts, samples_per_frame, bu
     pmc, src, r["kernel"], pmc_bid = load_pmc(config, dom)
     rp = load_rocprof(config, dom, build_id)
     if rp:  # the committed rocprofv3 summary of the same build: its average launch time beside the live one
-        r["rocprof"] = {"file": rp[0], "kernel": rp[1], "avg_launch_ms": rp[2], "live_over_rocprof": avg_ms / rp[2]}
+        r["rocprof"] = {"file": rp[0], "kernel": rp[1], "avg_launch_ms": rp[2], "live_over_rocprof": avg_ms / rp[2],
+                        "avg_launch_ms_all_frames": rp[3]}
     if pmc:
         n = pmc["dispatches"]
         # FETCH_SIZE (KB): MI355X_MICROARCH.md reads 1/2 of the bytes of wide (16 B/lane) coalesced streaming
