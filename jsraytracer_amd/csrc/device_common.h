@@ -702,16 +702,14 @@ JSRT_HD double sdf_cross(const T *k, F3 P) {
 // k[3..5]: 1/s when s is a power of two (x / s and x * (1 / s) are then the same rounding of the
 // same real number), else 0.
 template <class T>
+__device__ __forceinline__ float sdf_rep1(const T *k, int i, float p) {  // axis i, before sdf_xrep's `|| 0`
+    const double s = k[i], inv = k[3 + i], a = (double)p + s / 2;
+    const double q = floor(inv != 0.0 ? a * inv : a / s);
+    return (float)(to_precision8_sl(a - (q * s)) - s / 2);  // math.js:27 (branch-free form, js_number.h)
+}
+template <class T>
 __device__ __forceinline__ F3 sdf_xrep(const T *k, F3 P) {
-    const float pc[3] = {P.x, P.y, P.z};
-    float r[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const double s = k[i], inv = k[3 + i], a = (double)pc[i] + s / 2;
-        const double q = floor(inv != 0.0 ? a * inv : a / s);
-        r[i] = (float)(to_precision8_sl(a - (q * s)) - s / 2);  // math.js:27 (branch-free form, js_number.h)
-    }
-    return f3(r[0], or0(r[1]), or0(r[2]));
+    return f3(sdf_rep1(k, 0, P.x), or0(sdf_rep1(k, 1, P.y)), or0(sdf_rep1(k, 2, P.z)));
 }
 
 template <int N>
@@ -927,7 +925,8 @@ __device__ __forceinline__ SdfMD sdf_leaf_md(const DScene &S, const jsrt_rec_sdf
     return r;
 }
 
-__device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
+// hint (sdf_forms.h sdf_form_normal4): the root Difference's two operand distances at p, already evaluated
+__device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p, const double *hint = nullptr) {
     // Iterative post-order over the (binary) blend nodes; simple selector nodes are followed in place.
     struct Pending {
         int node;      // smooth node waiting for its children
@@ -955,6 +954,10 @@ __device__ __forceinline__ SdfMD sdf_material(const DScene &S, int root, F3 p) {
             continue;
         }
         case JSRT_SDF_DIFFERENCE:
+            if (hint && n == root) {
+                n = (hint[0] > -hint[1]) ? N.a : N.b;
+                continue;
+            }
             n = (sdf_node_dist(S, N.a, p) > -sdf_node_dist(S, N.b, p)) ? N.a : N.b;
             continue;
         case JSRT_SDF_ROUND:

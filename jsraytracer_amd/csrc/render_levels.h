@@ -427,8 +427,20 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
         // 72 -> 64 ms, r03_s14)
         const float step = (float)G.normal_step;
         double dd[4] = {0, 0, 0, 0};
+        bool four = false;  // the Menger form's four distances together (sdf_forms.h sdf_form_normal4)
+        double hab[2] = {0, 0};
+        if (S.sdf_all_forms) {
+            const int pc = S.sdf_range[2 * G.root];
+            for (;;) {  // waterfall over the lanes' programs (uniform pc)
+                const int pcu = uni(pc);
+                if (pc == pcu) {
+                    four = sdf_form_normal4(as_const(S.sdf_const), as_const(S.sdf_insn), pcu, pl, step, dd, hab);
+                    break;
+                }
+            }
+        }
 #pragma unroll 1
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < (four ? 0 : 4); ++k) {
             const F3 q = f3(pl.x + (k == 1 ? step : 0.0f), pl.y + (k == 2 ? step : 0.0f), pl.z + (k == 3 ? step : 0.0f));
             const double r = S.sdf_all_forms ? sdf_form_dist(S, G.root, q) : sdf_node_dist(S, G.root, q);
             dd[0] = k == 0 ? r : dd[0];
@@ -440,7 +452,7 @@ __device__ __forceinline__ void surface_data(const DScene &S, const Hit &h, F3 o
         const float nx = (float)((dd[1] - dist0) / G.normal_step);
         const float ny = (float)((dd[2] - dist0) / G.normal_step);
         const float nz = (float)((dd[3] - dist0) / G.normal_step);
-        const SdfMD md = sdf_material(S, G.root, pl);
+        const SdfMD md = sdf_material(S, G.root, pl, four ? hab : nullptr);
         if (md.has_bc) { basecolor = md.bc; has_bc = 1; }
         if (md.has_uv) { u = md.u; v = md.v; has_uv = 1; }
         nrm = normalized(f3(nx, ny, nz));

@@ -641,6 +641,23 @@ struct Loader {
         return {fb, (int32_t)S.sdf_insn.size()};
     }
 
+    // An SFORM_RUNION_DIFF's flags (the marker's b; sdf_forms.h sdf_form_normal4): 1 when the loop's matrix
+    // (XMATREP a, 3 rows of 4) is diagonal -- every off-diagonal entry a zero of either sign, the translations +0
+    // (their bits), the diagonal below 1e30 in magnitude -- so each coordinate's chain through the loop depends on
+    // that coordinate alone.  JSRT_SDF_N4=0 clears it (A/B).
+    int32_t runion_flags(const SdfInsn *R) const {
+        const char *knob = getenv("JSRT_SDF_N4");
+        if (knob && knob[0] == '0') return 0;
+        if (R[4].a < 0 || R[4].a + 12 > (int32_t)S.sdf_const.size()) return 0;
+        const double *m = S.sdf_const.data() + R[4].a;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) {
+                const double v = m[4 * r + c];
+                if (c == 3 ? !(v == 0.0 && !signbit(v)) : c == r ? !(fabs(v) < 1e30) : v != 0.0) return 0;
+            }
+        return 1;
+    }
+
     // Program shapes with straight-line device code (sdf_forms.h): a recognised fused range gets a copy
     // prefixed by an SOP_FORM marker (the form reads its constants from the copied instructions).
     std::pair<int32_t, int32_t> match_sdf_forms(int32_t begin, int32_t end) {
@@ -704,6 +721,7 @@ struct Loader {
             }
         }
         if (!form) return {begin, end};
+        if (form == SFORM_RUNION_DIFF) fflags = runion_flags(I + 1);
         const int32_t fb = (int32_t)S.sdf_insn.size();
         S.sdf_insn.push_back(SdfInsn{SOP_FORM, form, fflags, fpad});
         for (int32_t i = 0; i < n; ++i) {

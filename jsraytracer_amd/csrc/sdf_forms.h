@@ -48,6 +48,60 @@ __device__ __forceinline__ double sdf_form_runion_diff(const KT *K, const CT *co
     return js_max(d0, -d1);
 }
 
+// SDFGeometry.materialData's four distances (sdf.js:41-47: at P and at P + step along each axis, every other
+// coordinate + 0.0f) of an SFORM_RUNION_DIFF whose loop matrix is diagonal (marker b & 1, scene_load.cpp
+// runion_flags) and whose unions are both the Menger cross (MINBOX pad).  With finite coordinates the matrix row i
+// is x_i m_ii + 0.0 (the zero products and the +0 translation leave a non-zero product and turn a zero sum into
+// +0, as the reference's sum does) and the repetition is per axis, so coordinate i's chain through the loop
+// depends on coordinate i alone: the four points share it, and each axis runs two chains (the point's and the
+// offset one) instead of four -- half the toPrecision(8) steps.  The boxes, the crosses and the min / max run per
+// point as sdf_form_runion_diff runs them.  -0 and +0 give the same chain (every use is |x| or x + c).  Returns
+// false (nothing written) unless every coordinate entering a matrix row is finite: the caller then evaluates
+// the four points one by one.  ab: the box's and the union's distances at P, which DifferenceSDF.getMaterialData
+// compares (sdf.js:117-125): the child nodes' own programs are the same box and SFORM_RUNION code.
+template <class KT, class CT>
+__device__ __forceinline__ bool sdf_form_normal4(const KT *K, const CT *code, int pc, F3 P, float step, double dd[4],
+                                                 double ab[2]) {
+    if (!(uni(code[pc].op) == SOP_FORM && uni(code[pc].a) == SFORM_RUNION_DIFF && (uni(code[pc].b) & 1) &&
+          uni(code[pc + 3].pad) && uni(code[pc + 7].pad)))
+        return false;
+    const int r = pc + 2;  // the SFORM_RUNION at [r, r + 10): MINBOX r + 1, LOOP r + 3, XMATREP r + 4, MINBOX r + 5
+    const int bx = uni(code[pc + 1].a), u0 = uni(code[r + 1].a), iters = uni(code[r + 3].a);
+    const int xm = uni(code[r + 4].a), xs = uni(code[r + 4].b), xr = uni(code[r + 4].pad), u1 = uni(code[r + 5].a);
+    float cx[2] = {P.x + 0.0f, P.x + step}, cy[2] = {P.y + 0.0f, P.y + step}, cz[2] = {P.z + 0.0f, P.z + step};
+    double d0[4], d1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const F3 q = f3(cx[k == 1], cy[k == 2], cz[k == 3]);
+        d0[k] = sdf_box(K + bx, q);
+        d1[k] = sdf_cross(K + u0, q);
+    }
+    bool fin = true;
+    double sc = 1.0;
+    const double m0 = K[xm], m5 = K[xm + 5], m10 = K[xm + 10];
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            fin = fin && fabsf(cx[j]) <= __FLT_MAX__ && fabsf(cy[j]) <= __FLT_MAX__ && fabsf(cz[j]) <= __FLT_MAX__;
+            cx[j] = sdf_rep1(K + xr, 0, (float)((double)cx[j] * m0 + 0.0));
+            cy[j] = or0(sdf_rep1(K + xr, 1, (float)((double)cy[j] * m5 + 0.0)));
+            cz[j] = or0(sdf_rep1(K + xr, 2, (float)((double)cz[j] * m10 + 0.0)));
+        }
+        sc = sc * (1.0 * (1.0 * K[xs]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double d = sdf_cross(K + u1, f3(cx[k == 1], cy[k == 2], cz[k == 3]));
+            d1[k] = js_min(d1[k], d * sc);
+        }
+    }
+    if (!fin) return false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dd[k] = js_max(d0[k], -d1[k]);
+    ab[0] = d0[0];  // the Difference's two operands at P: getMaterialData's choice (sdf_material's hint)
+    ab[1] = d1[0];
+    return true;
+}
+
 // One primitive of a form: BOX / SPHERE / TETRA at instruction `pc` (the VM's cases, sdf.js:232-234,
 // 276-279, 305-308), the opcode read uniform.
 template <class KT, class CT>
