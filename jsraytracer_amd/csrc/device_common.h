@@ -1667,8 +1667,11 @@ __device__ __forceinline__ void march_step(const DScene &S, MarchState &m, doubl
 #ifndef JSRT_MARCH_STEPS
 #define JSRT_MARCH_STEPS 8
 #endif
-#ifndef JSRT_MARCH_KEEP
-#define JSRT_MARCH_KEEP 56
+#ifndef JSRT_MARCH_KEEP  // closest-hit marches (k_extend_q)
+#define JSRT_MARCH_KEEP 48
+#endif
+#ifndef JSRT_MARCH_KEEP_ANY  // shadow marches (k_shadow_cast)
+#define JSRT_MARCH_KEEP_ANY 36
 #endif
 template <int PF, bool ANY, bool FO, class Src>
 __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, uint32_t count, double minD,
@@ -1711,13 +1714,16 @@ __device__ __forceinline__ void persistent_cast(const DScene &S, uint32_t *ctr, 
         // the refill (ballot, atomic, ray loads) and the root walk of the lanes that finished run once per
         // round instead of once per step, at the price of a finished lane idling for the rest of its round
         // (SDF_Menger: 1 step 118.8 M/s, 2 steps 150.7 / 147.6, 4 steps 127.6, 8 steps 99.1; up to 8 steps while
-        // >= 56 lanes march 151.7, >= 48 149.4; profiles/r04_s13_ab.txt, r04_s14_ab.txt)
+        // >= 56 lanes march 151.7, >= 48 149.4; profiles/r04_s13_ab.txt, r04_s14_ab.txt.  Round 6, with the
+        // evaluation ~1.5x cheaper, the refill costs relatively more: keep 56 / 48 / 40 / 32 / 24 read 225.8 / 239.1 /
+        // 239.3 / 232.7 / 223.3 M/s, the closest-hit march best at 48 (k_extend_q 75.0 ms) and the shadow march at
+        // 32-40 (k_shadow_cast 40.3 ms); profiles/r06_s19_march_knobs_menger.txt, r06_s20_march_keep_menger.txt)
         if (__any(have && m.marching)) {
 #pragma unroll 1
             for (int k = 0; k < JSRT_MARCH_STEPS; ++k) {
                 if (have && m.marching) march_step<ANY, FO>(S, m, minD, maxD);
                 const uint64_t mb = __ballot(have && m.marching);
-                if (!mb || (k > 0 && __popcll(mb) < JSRT_MARCH_KEEP)) break;
+                if (!mb || (k > 0 && __popcll(mb) < (ANY ? JSRT_MARCH_KEEP_ANY : JSRT_MARCH_KEEP))) break;
             }
         }
     }
