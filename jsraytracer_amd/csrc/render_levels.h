@@ -37,8 +37,8 @@
 #ifndef JSRT_MARCH_OCC  // min waves per SIMD of the persistent SDF marches (k_extend_q, k_shadow_cast)
 #define JSRT_MARCH_OCC 1
 #endif
-#ifndef JSRT_EXTEND_OCC_FLAT  // analytic profile: 6 fits without spills (cornell +1 %, r02_s20)
-#define JSRT_EXTEND_OCC_FLAT 6
+#ifndef JSRT_EXTEND_OCC_FLAT  // analytic profile: 8 waves (round 6: k_extend 30.37 -> 29.74 ms, 5 waves 30.35,
+#define JSRT_EXTEND_OCC_FLAT 8   // profiles/r06_s21_occ_cornell.txt; round 2 had 6 beat 5, r02_s20)
 #endif
 // optional waves-per-EU window (min, max) per kernel for A/B occupancy experiments
 #ifdef JSRT_SHADOW_WPE
