@@ -17,6 +17,9 @@
 #ifndef JSRT_SHADE_OCC  // min waves per SIMD requested for k_shade: 4 (SDF 167 -> 128 VGPRs) = Menger +5 %, r03_s34
 #define JSRT_SHADE_OCC 4
 #endif
+#ifndef JSRT_SHADE_OCC_SDF  // SDF profiles: 3 waves (round 6, after the four-distance normal: Menger k_shade 28.5 ->
+#define JSRT_SHADE_OCC_SDF 3  // 25.1 ms, 5 waves 34.9; profiles/r06_s25_shade_occ_menger.txt)
+#endif
 #ifndef JSRT_SHADE_OCC_FLAT  // analytic profile: 5 waves (95 VGPRs, 8 spilled) beat 4 (105): cornell +2.4 %, r03_s14
 #define JSRT_SHADE_OCC_FLAT 5
 #endif
@@ -857,7 +860,8 @@ __device__ __forceinline__ void stab_bind(DScene &SL, const uint4 *lds, bool sha
 // STAGE (flat scenes whose shading tables fit, DScene::stab): the tables are copied into LDS by every block, so a
 // hit's dependent record chain (prim -> shading matrix / material -> colour constants) is LDS round trips
 template <int PF, bool CHAIN, bool STAGE>
-__global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
+__global__ __launch_bounds__(256, PF == PF_ANALYTIC ? JSRT_SHADE_OCC_FLAT
+                                                    : (PF & PF_SDF) ? JSRT_SHADE_OCC_SDF : JSRT_SHADE_OCC) SHADE_ATTR void k_shade(
     DScene S, WArgs W, int L, int child_depth) {
     XST_BEGIN
     const uint32_t t0 = blockIdx.x * 256, tt = t0 + threadIdx.x;
