@@ -59,3 +59,30 @@ def test_gpu_sdf_distance_rejects_non_sdf_object(jr):
     sc = jr.Scene(pyoracle.golden_scene("SDF_Menger"), device=0)
     with pytest.raises(jr.JsrtError, match="not an SDFGeometry"):
         sc.sdf_distance(0, np.zeros((1, 4), np.float32))  # object 0 is the floor plane
+
+
+def test_gpu_menger_material_data_dense_against_oracle(jr):
+    """SDF_Menger's materialData on 16,384 rays from inside and around the sponge (hits on the hole walls at every
+    level), against the oracle: the four normal distances sharing each axis's transform/repetition chain and
+    getMaterialData's choice from them (sdf_forms.h sdf_form_normal4) must give every f32 bit of the normal,
+    position and basecolour.  The sponge: Mat4.translation([-3.5, 0.5, -3.5]) x rotationY(-0.15) of a unit box."""
+    blob = pyoracle.golden_scene("SDF_Menger")
+    rng = np.random.default_rng(29)
+    c = np.array([-3.5, 0.5, -3.5])
+    o = (c + rng.uniform(-1.4, 1.4, (16384, 3))).astype(np.float32)
+    d = rng.normal(size=(16384, 3))
+    d[:4096] = np.round(d[:4096] * 2) / 2 + 1e-3
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    rays = np.concatenate([o, d], 1)
+    want = pyoracle.material_data(blob, rays)
+    sc = jr.Scene(blob, device=0)
+    try:
+        got = sc.material_data(rays)
+    finally:
+        sc.close()
+    assert np.array_equal(got["obj"], want["obj"])
+    hit = want["obj"] == 1
+    assert hit.sum() > 5000
+    for f, cols in (("normal", 4), ("position", 4), ("basecolor", 3)):
+        bad = _diff_rows(got[f][hit, :cols], want[f][hit, :cols])
+        assert bad.size == 0, f"{f}: {bad.size} of {int(hit.sum())} differ, first {got[f][hit][bad[0]]} vs {want[f][hit][bad[0]]}"
